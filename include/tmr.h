@@ -1,0 +1,160 @@
+/*
+ * tmr.h -- C ABI of libtmr.so, the MI355X-native TMR hot path.
+ *
+ * Every entry point replaces one reference operation on the path named by
+ * BASELINE.json north_star (file:line into mFinn27/Template-Matching-and-
+ * Regression-MapReduce @ 2026-01-16).  The reference
+ * is pure Python over ATen/torchvision, so the "FFI" a maintainer binds is
+ * Python ctypes (INTEGRATION.md shows the stub); no torch types cross this
+ * boundary.
+ *
+ * Conventions
+ *  - All tensor pointers are DEVICE pointers owned by the caller; the library
+ *    never allocates or frees device memory.  fp32, NCHW, contiguous.
+ *  - Every call is asynchronous on `stream` (a hipStream_t, passed as void*;
+ *    NULL = the null stream) and returns 0 or a negative TMR_E* code; nothing
+ *    throws across the ABI.  tmr_strerror() names the code.
+ *  - No global mutable state: calls are reentrant across streams/devices.
+ *  - "units" are (image, exemplar) matching units, described by a device
+ *    array of tmr_unit_t built on the host (the reference sizes templates on
+ *    the host too: template_matching.py:56-73 runs Python math on 0-d
+ *    tensors).
+ */
+#ifndef TMR_H_
+#define TMR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMR_ABI_VERSION 1
+
+enum {
+    TMR_OK = 0,
+    TMR_E_INVALID = -1,    /* bad argument / shape */
+    TMR_E_HIP = -2,        /* a HIP runtime error (launch failure) */
+    TMR_E_UNSUPPORTED = -3 /* configuration not built into this library */
+};
+
+enum { TMR_TEMPLATE_ROI_ALIGN = 0, TMR_TEMPLATE_PROTOTYPE = 1 };
+
+/* One (image, exemplar) matching unit.  Built by the host from the exemplar
+ * box exactly as models/template_matching.py:43-76 does. */
+typedef struct tmr_unit {
+    int32_t image;         /* index into the feature batch                        */
+    int32_t type;          /* TMR_TEMPLATE_*                                      */
+    int32_t ht, wt;        /* template size (odd; 1x1 for prototype)              */
+    float roi[4];          /* roi_align box in feature px (x1,y1,x2,y2), :61-63   */
+    int32_t pbox[4];       /* prototype snapped box (x1,y1,x2,y2), :49-50         */
+    int64_t tmpl_offset;   /* float offset of this unit's [C,ht,wt] template      */
+} tmr_unit_t;
+
+/* Per-unit peak-finder parameters (utils/TM_utils.py:236-278). */
+typedef struct tmr_peak_param {
+    float thr;             /* fl32(cls_ths), compared p >= thr (:254)             */
+    float scale_w, scale_h;/* decode scale: clamped exemplar w,h or 1 (:239-243)  */
+    int32_t mask;          /* 9-bit 3x3 kernel, bit (dy+1)*3+(dx+1) (:363-377)    */
+    int32_t mode;          /* 0 box regression, 1 ablation_c, 2 no regression      */
+    int32_t pad_;
+} tmr_peak_param_t;
+
+int tmr_version(void);
+const char *tmr_strerror(int rc);
+
+/* ---- weights ---------------------------------------------------------
+ * Pack conv weights W[N][C][ks][ks] (PyTorch layout) for the MFMA conv
+ * kernels: wpack is [ceil(N/128)][ceil(C/cc)][ks*ks][cc][128] fp32, zero
+ * padded.  Size in floats from tmr_conv_pack_size().  Replaces nothing in the
+ * reference (a derived cache of nn.Conv2d.weight, regression_head.py:7 and
+ * matching_net.py:27-30). */
+int64_t tmr_conv_pack_size(int N, int C, int ks);
+int tmr_conv_pack(const float *w, int N, int C, int ks, float *wpack, void *stream);
+
+/* ---- (a2+a3) bilinear x2 upsample fused into the 1x1 input projection -----
+ * fp[b] = W_proj * up2x(feat[b]) + bias   (models/matching_net.py:50-51,56)
+ * feat [B,Cin,Hin,Win]; fp [B,N,H,W] with H=2*Hin (upsample!=0) or H=Hin.
+ * f0 (nullable) receives up2x(feat) [B,Cin,H,W] (the API output f[0], :81). */
+int tmr_upsample_proj(const float *feat, int B, int Cin, int Hin, int Win, int upsample,
+                      const float *wpack, const float *bias, int N, float *fp, float *f0,
+                      void *stream);
+
+/* ---- (a6+a7+a8) exemplar templates --------------------------------------
+ * torchvision.ops.roi_align(f, [roi], (ht,wt), aligned=True) per unit
+ * (models/template_matching.py:75) or the prototype AdaptiveAvgPool2d(1)
+ * (:52).  f [B,C,H,W]; templates written at units[u].tmpl_offset as [C,ht,wt]. */
+int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *units, int U,
+                  int max_ht, int max_wt, float *templates, void *stream);
+
+/* ---- (a9+a4) depthwise cross-correlation + pad + scale -------------------
+ * out[u] = pad(conv2d(f[img(u)], T_u, groups=C) / fl32(ht*wt)) * scale
+ * (models/template_matching.py:23-41, :97).  scale is a device scalar.
+ * squeeze!=0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and
+ * `work` must hold U*C*H*W floats; otherwise out is [U,C,H,W] and work may
+ * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79). */
+int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
+              const tmr_unit_t *units, int U, int max_ht, int max_wt, const float *scale,
+              int squeeze, float *out, float *relu_out, float *work, void *stream);
+
+/* ---- (a10+a11+a12) conv stack ---------------------------------------------
+ * Implicit-GEMM kxk conv over the virtual channel concat
+ *   x_u = cat([src0[unit_image[u]] (C0 ch), src1[u] (C1 ch)])   (matching_net.py:64)
+ * with bias and optional LeakyReLU(0.01) (regression_head.py:7-8), fp32 MFMA.
+ * unit_image (device int32[U]) may be NULL (identity).
+ * tmr_conv_store: out [U,N,H,W].
+ * tmr_conv_heads: the fused decoder+1x1-head epilogue; out is never stored:
+ *   partials[t][j][u][h][w] += sum_{n in tile t} act(conv)[n] * headw[n][j], j<5
+ *   (headw [ceil(N/128)*128][5] fp32, zero padded; j 0-3 = ltrbs_head,
+ *   4 = objectness_head,
+ *   regression_head.py:31,50) and tmr_heads_reduce() adds the head biases. */
+int tmr_conv_store(const float *src0, int C0, const int32_t *unit_image, const float *src1,
+                   int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
+                   int ks, int leaky, float *out, void *stream);
+int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_image, const float *src1,
+                   int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
+                   int ks, int leaky, const float *headw, float *partials, void *stream);
+int64_t tmr_heads_partials_size(int N, int U, int H, int W);
+/* o [U,1,H,W] = head_bias[4] + sum_t partials[t][4];  b [U,4,H,W] (nullable) =
+ * head_bias[j] + sum_t partials[t][j]. */
+int tmr_heads_reduce(const float *partials, int N, int U, int H, int W, const float *head_bias,
+                     float *o, float *b, void *stream);
+
+/* ---- (a14-a16) peak finder + box decode ------------------------------------
+ * Get_pred_boxes per unit (utils/TM_utils.py:245-282): p = sigmoid(o) (or o
+ * itself when input_is_prob), masked 3x3 local max with zero padding,
+ * p >= thr, row-major compaction (no cap), decode.  Outputs per unit u at
+ * stride cap = H*W: logits[(u*cap+i)*2] = (p, 0) (TM_utils.py:260-261),
+ * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u].
+ * prob [U,H,W] receives the probability map (required). */
+int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H, int W,
+                     const tmr_peak_param_t *params, float *prob, float *logits, float *box,
+                     float *ref, int32_t *counts, void *stream);
+
+/* ---- (a17-a19) per-image greedy NMS over the exemplar-ordered union --------
+ * torchvision.ops.nms (utils/TM_utils.py:317-323) on, per image g, the
+ * concatenation (in unit order seg_units[g] .. seg_units[g+1]-1) of each
+ * unit's candidates, or of the dummy row [0,0,1e-14,1e-14]/score 0 when the
+ * unit has none (TM_utils.py:288-291).  Unit u's counts[u] candidates start
+ * at row unit_off[u] (device int64[U]) of logits [.,2] / box [.,4] /
+ * ref [.,2]; the score is logits[.,0] (:319).  seg_units (device int32[G+1]),
+ * cand_off (device int64[G+1], the offsets of those unions) and mask_off
+ * (device int64[G+1], prefix sums of n_g*ceil(n_g/64)) are computed on the
+ * host from the candidate counts (one sync, as the reference's torch.where).
+ * Outputs are written per image at cand_off[g]: keep-ordered logits [n,2] =
+ * (score, 0), boxes [n,4], refs [n,2], optionally the keep indices (int64,
+ * local to the image's union, = torchvision's return value) and kept[g].
+ * `work` holds
+ * tmr_nms_work_size(total_cand, mask_off[G]) bytes. */
+int64_t tmr_nms_work_size(int64_t total_cand, int64_t mask_words);
+int tmr_nms(const float *logits, const float *box, const float *ref, const int32_t *counts,
+            const int64_t *unit_off, const int32_t *seg_units, const int64_t *cand_off,
+            const int64_t *mask_off,
+            int G, int64_t total_cand, int64_t max_cand, double iou_threshold,
+            float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
+            int32_t *kept, void *work, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMR_H_ */

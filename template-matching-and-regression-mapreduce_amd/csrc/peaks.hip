@@ -1,0 +1,121 @@
+// Peak finder + box decode (gfx950): Get_pred_boxes for one level
+// (utils/TM_utils.py:245-282) with adaptive_kernel_generater's 3x3 mask
+// (:363-377) and custom_shape_3x3_maxpool2d (:337-361, zero padding).
+//
+//   1. prob_kernel:  p = sigmoid(o) (near-correctly rounded) or p = o.
+//   2. peaks_kernel: one 1024-thread workgroup per unit; each lane owns a
+//      contiguous run of pixels, flags p >= thr && p == masked 3x3 max,
+//      a workgroup prefix sum gives each candidate its row-major slot
+//      (torch.where order, no cap), and the candidate is decoded in place:
+//      ref = (x/W, y/H); xy = ref + r[:2]*s; wh = exp(r[2:])*(bw,bh);
+//      box = (xy - wh/2, xy + wh/2).
+// Built with -ffp-contract=off so every op is separately rounded as in the
+// reference's elementwise torch ops.
+#include "tmr_common.h"
+
+namespace {
+
+constexpr int NT = 1024;
+
+__global__ void prob_kernel(const float *__restrict__ o, int64_t n, int is_prob,
+                            float *__restrict__ p) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = o[i];
+    p[i] = is_prob ? v : tmr_sigmoid_cr(v);
+}
+
+__device__ __forceinline__ bool is_peak(const float *__restrict__ p, int H, int W, int y, int x,
+                                        int mask, float thr) {
+    const float v = p[y * W + x];
+    if (!(v >= thr)) return false;
+    float mx = 0.0f;
+    bool first = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (!((mask >> ((dy + 1) * 3 + dx + 1)) & 1)) continue;
+            const int yy = y + dy, xx = x + dx;
+            const float q = (yy < 0 || yy >= H || xx < 0 || xx >= W) ? 0.0f : p[yy * W + xx];
+            if (first || q > mx) { mx = q; first = false; }
+        }
+    return mx == v;
+}
+
+__global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ prob,
+                                                   const float *__restrict__ reg, int H, int W,
+                                                   const tmr_peak_param_t *__restrict__ params,
+                                                   float *__restrict__ logits, float *__restrict__ box,
+                                                   float *__restrict__ ref, int32_t *__restrict__ counts) {
+    __shared__ int wsum[NT / 64];
+    const int u = blockIdx.x;
+    const tmr_peak_param_t pp = params[u];
+    const int HW = H * W;
+    const float *p = prob + (size_t)u * HW;
+    const int per = (HW + NT - 1) / NT;
+    const int beg = min(threadIdx.x * per, HW), end = min(beg + per, HW);
+    // pass 1: count (bits of up to 64 owned pixels kept in a register mask)
+    int cnt = 0;
+    for (int i = beg; i < end; ++i) cnt += is_peak(p, H, W, i / W, i % W, pp.mask, pp.thr);
+    // workgroup exclusive scan
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int wbase = 0, total = 0;
+    for (int k = 0; k < NT / 64; ++k) {
+        int s = wsum[k];
+        if (k < wave) wbase += s;
+        total += s;
+    }
+    int pos = wbase + incl - cnt;
+    if (threadIdx.x == 0) counts[u] = total;
+    if (cnt == 0) return;
+    const size_t cap = (size_t)HW;
+    const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
+    for (int i = beg; i < end; ++i) {
+        const int y = i / W, x = i % W;
+        if (!is_peak(p, H, W, y, x, pp.mask, pp.thr)) continue;
+        const size_t k = (size_t)u * cap + pos++;
+        const float v = p[i];
+        const float rx = (float)x / (float)W, ry = (float)y / (float)H;
+        float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+        if (pp.mode != 2 && r) {
+            r0 = r[i]; r1 = r[HW + i]; r2 = r[2 * HW + i]; r3 = r[3 * HW + i];
+        }
+        const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
+        const float cx = rx + r0 * sx, cy = ry + r1 * sy;
+        const float w = tmr_expf_cr(r2) * pp.scale_w, h = tmr_expf_cr(r3) * pp.scale_h;
+        const float hw2 = w / 2.0f, hh2 = h / 2.0f;
+        logits[2 * k + 0] = v;
+        logits[2 * k + 1] = 0.0f;
+        box[4 * k + 0] = cx - hw2;
+        box[4 * k + 1] = cy - hh2;
+        box[4 * k + 2] = cx + hw2;
+        box[4 * k + 3] = cy + hh2;
+        ref[2 * k + 0] = rx;
+        ref[2 * k + 1] = ry;
+    }
+}
+
+}  // namespace
+
+extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H,
+                                int W, const tmr_peak_param_t *params, float *prob, float *logits,
+                                float *box, float *ref, int32_t *counts, void *stream) {
+    TMR_REQUIRE(o && params && prob && logits && box && ref && counts && U > 0 && H > 0 && W > 0);
+    hipStream_t s = tmr_stream(stream);
+    int64_t n = (int64_t)U * H * W;
+    hipLaunchKernelGGL(prob_kernel, dim3((unsigned)tmr_cdiv(n, 256)), dim3(256), 0, s, o, n,
+                       input_is_prob, prob);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(peaks_kernel, dim3(U), dim3(NT), 0, s, prob, reg, H, W, params, logits, box, ref,
+                       counts);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}

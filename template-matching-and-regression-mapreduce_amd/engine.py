@@ -1,0 +1,340 @@
+"""Batched native pipeline of the TMR hot path.
+
+``TMREngine`` runs, for a batch of B images x E exemplars (U = B*E matching
+units), everything after the frozen backbone on libtmr.so:
+
+  upsample x2 + input_proj       tmr_upsample_proj   matching_net.py:50-56
+  exemplar templates             tmr_templates       template_matching.py:55-76
+  depthwise xcorr + pad + scale  tmr_xcorr           template_matching.py:23-41,97
+  decoders + heads (fused)       tmr_conv_heads      regression_head.py, matching_net.py:63-75
+  peaks + decode                 tmr_peaks_decode    TM_utils.py:224-305
+  NMS over the exemplar union    tmr_nms             TM_utils.py:307-323, demo.py:106-130
+
+The projection is computed once per image and shared by its E units; the
+reference recomputes it per exemplar (demo.py:111, trainer.py:96-97), with
+bit-identical results, so sharing it changes no output.
+
+Weights are the reference's state_dict tensors (SURVEY.md §8b keys); packed
+MFMA layouts are derived caches, rebuilt when a parameter changes.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import host
+from ._lib import TMRError, call, load, ptr, require_gpu, stream
+
+NHEAD = 5
+
+
+@dataclass
+class PathConfig:
+    """The matching_net flags on the path (matching_net.py:13-39)."""
+    emb_dim: int = 512
+    fusion: bool = True
+    squeeze: bool = False
+    box_reg: bool = True
+    template_type: str = "roi_align"
+    feature_upsample: bool = True
+    decoder_num_layer: int = 1
+    decoder_kernel_size: int = 3
+    no_matcher: bool = False
+
+    @classmethod
+    def from_args(cls, args) -> "PathConfig":
+        return cls(emb_dim=args.emb_dim, fusion=bool(args.fusion), squeeze=bool(args.squeeze),
+                   box_reg=not args.ablation_no_box_regression, template_type=args.template_type,
+                   feature_upsample=bool(args.feature_upsample),
+                   decoder_num_layer=args.decoder_num_layer,
+                   decoder_kernel_size=args.decoder_kernel_size, no_matcher=bool(args.no_matcher))
+
+
+def _version_key(ts: Sequence[torch.Tensor]):
+    return tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
+
+
+class _PackCache:
+    """Derived weight layouts keyed on the parameters' storage and version."""
+
+    def __init__(self):
+        self._d: Dict[str, Tuple[tuple, object]] = {}
+
+    def get(self, name: str, tensors: Sequence[torch.Tensor], build):
+        key = _version_key(tensors)
+        hit = self._d.get(name)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        val = build()
+        self._d[name] = (key, val)
+        return val
+
+
+def pack_conv(w: torch.Tensor) -> torch.Tensor:
+    """[N,C,ks,ks] fp32 -> tmr_conv_pack layout (include/tmr.h)."""
+    require_gpu(w, "conv weight")
+    w = w.detach().float().contiguous()
+    N, C, ks, ks2 = w.shape
+    if ks != ks2:
+        raise TMRError("square kernels only (regression_head.py:7)")
+    n = load().tmr_conv_pack_size(N, C, ks)
+    if n <= 0:
+        raise TMRError(f"unsupported conv shape {tuple(w.shape)}")
+    out = torch.empty(n, device=w.device, dtype=torch.float32)
+    call("tmr_conv_pack", ptr(w), N, C, ks, ptr(out), stream())
+    return out
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool, packed=None):
+    """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the MFMA kernel."""
+    require_gpu(x, "conv input")
+    x = x.float().contiguous()
+    U, C, H, W = x.shape
+    N = w.shape[0]
+    if w.shape[1] != C:
+        raise TMRError(f"conv expects {w.shape[1]} input channels, got {C}")
+    wp = packed if packed is not None else pack_conv(w)
+    out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
+    call("tmr_conv_store", ptr(x), C, None, None, 0, U, H, W, ptr(wp),
+         ptr(b.detach().float().contiguous()), N, w.shape[-1], int(leaky), ptr(out), stream())
+    return out
+
+
+def _units_to_device(units: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(units.view(np.uint8).copy()).to(device, non_blocking=False)
+
+
+class TMREngine:
+    """Native forward + post-processing over (image, exemplar) units."""
+
+    def __init__(self, params: Dict[str, torch.Tensor], cfg: PathConfig):
+        self.P = params
+        self.cfg = cfg
+        self._cache = _PackCache()
+        if cfg.decoder_kernel_size not in (1, 3, 5, 7):
+            raise TMRError("decoder_kernel_size must be 1, 3, 5 or 7")
+
+    # ------------------------------------------------------------ weights
+    def _dec_layers(self, pre: str):
+        out = []
+        for l in range(self.cfg.decoder_num_layer):
+            out.append((self.P[f"{pre}.layer.{2 * l}.weight"], self.P[f"{pre}.layer.{2 * l}.bias"]))
+        return out
+
+    def _proj(self):
+        w, b = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
+        wp = self._cache.get("proj", [w], lambda: pack_conv(w))
+        return wp, b.detach().float().contiguous(), w.shape[0], w.shape[1]
+
+    def _fused_decoders(self):
+        """Layer-0 weights of decoder_b and decoder_o concatenated along N, with
+        the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders)."""
+        cfg = self.cfg
+        layers = ([self._dec_layers("decoder_b")[0]] if cfg.box_reg else []) + \
+            [self._dec_layers("decoder_o")[0]]
+        ow, ob = self.P["objectness_head.head.0.weight"], self.P["objectness_head.head.0.bias"]
+        heads = [ow, ob]
+        if cfg.box_reg:
+            lw, lb = self.P["ltrbs_head.head.0.weight"], self.P["ltrbs_head.head.0.bias"]
+            heads += [lw, lb]
+        tensors = [t for wb in layers for t in wb] + heads
+
+        def build():
+            W = torch.cat([w.detach().float() for w, _ in layers], 0).contiguous()
+            Bv = torch.cat([b.detach().float() for _, b in layers], 0).contiguous()
+            N = W.shape[0]
+            npad = ((N + 127) // 128) * 128
+            hw = torch.zeros((npad, NHEAD), device=W.device, dtype=torch.float32)
+            hb = torch.zeros(NHEAD, device=W.device, dtype=torch.float32)
+            n0 = 0
+            if cfg.box_reg:
+                nb = layers[0][0].shape[0]
+                hw[:nb, 0:4] = lw.detach().float().reshape(4, nb).t()
+                hb[0:4] = lb.detach().float()
+                n0 = nb
+            no = layers[-1][0].shape[0]
+            hw[n0:n0 + no, 4] = ow.detach().float().reshape(no)
+            hb[4] = ob.detach().float().reshape(())
+            return pack_conv(W), Bv, N, W.shape[1], hw.contiguous(), hb.contiguous()
+
+        return self._cache.get("fused_dec", tensors, build)
+
+    # ------------------------------------------------------------ forward
+    def project(self, feats: torch.Tensor, want_f0: bool = False):
+        """fp = input_proj(up2x(feats)) [B,emb,H,W] (+ f0 = up2x(feats))."""
+        require_gpu(feats, "features")
+        feats = feats.float().contiguous()
+        B, Cin, Hin, Win = feats.shape
+        wp, b, N, Cw = self._proj()
+        if Cw != Cin:
+            raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
+        up = self.cfg.feature_upsample
+        H, W = (2 * Hin, 2 * Win) if up else (Hin, Win)
+        fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
+        f0 = None
+        if want_f0:
+            f0 = torch.empty((B, Cin, H, W), device=feats.device, dtype=torch.float32) if up else feats
+        call("tmr_upsample_proj", ptr(feats), B, Cin, Hin, Win, int(up), ptr(wp), ptr(b), N,
+             ptr(fp), ptr(f0) if (want_f0 and up) else None, stream())
+        return fp, f0
+
+    def match(self, fp: torch.Tensor, unit_image: Sequence[int], unit_boxes: np.ndarray,
+              want_relu: bool = False):
+        """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu)."""
+        B, C, H, W = fp.shape
+        U = len(unit_image)
+        cfg = self.cfg
+        units, tfl, mh, mw = host.build_units(unit_boxes, unit_image, H, W, C, cfg.template_type)
+        dev = fp.device
+        units_d = _units_to_device(units, dev)
+        tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
+        call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
+        Co = 1 if cfg.squeeze else C
+        out = torch.empty((U, Co, H, W), device=dev, dtype=torch.float32)
+        relu = torch.empty_like(out) if want_relu else None
+        work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
+        scale = self.P["matcher.scale"].detach().float().contiguous()
+        call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), U, mh, mw, ptr(scale),
+             int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
+             ptr(work) if work is not None else None, stream())
+        return out, relu
+
+    def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int]):
+        """Decoders + heads over cat([fp[img(u)], f_TM[u]]) -> o [U,1,H,W], b [U,4,H,W]|None."""
+        cfg = self.cfg
+        U, C1, H, W = f_tm.shape
+        dev = f_tm.device
+        C0 = fp.shape[1] if cfg.fusion else 0
+        ui = torch.as_tensor(np.asarray(unit_image, np.int32), device=dev)
+        src0 = fp if cfg.fusion else None
+        if cfg.decoder_num_layer == 1:
+            wp, bias, N, Cw, hw, hb = self._fused_decoders()
+            if Cw != C0 + C1:
+                raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
+            nparts = load().tmr_heads_partials_size(N, U, H, W)
+            part = torch.empty(nparts, device=dev, dtype=torch.float32)
+            call("tmr_conv_heads", ptr(src0) if src0 is not None else None, C0, ptr(ui), ptr(f_tm),
+                 C1, U, H, W, ptr(wp), ptr(bias), N, cfg.decoder_kernel_size, 1, ptr(hw), ptr(part),
+                 stream())
+            o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
+            b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
+            call("tmr_heads_reduce", ptr(part), N, U, H, W, ptr(hb), ptr(o),
+                 ptr(b) if b is not None else None, stream())
+            return o, b
+        # general depth: per-decoder conv stack, heads as 1x1 convs
+        x0 = torch.cat([fp.index_select(0, ui.long()), f_tm], 1) if cfg.fusion else f_tm
+        res = {}
+        for pre in (["decoder_b"] if cfg.box_reg else []) + ["decoder_o"]:
+            x = x0
+            for l, (w, bb) in enumerate(self._dec_layers(pre)):
+                wp = self._cache.get(f"{pre}.{l}", [w], lambda w=w: pack_conv(w))
+                x = conv2d(x, w, bb, True, wp)
+            res[pre] = x
+        ow, ob = self.P["objectness_head.head.0.weight"], self.P["objectness_head.head.0.bias"]
+        o = conv2d(res["decoder_o"], ow, ob, False,
+                   self._cache.get("obj", [ow], lambda: pack_conv(ow)))
+        b = None
+        if cfg.box_reg:
+            lw, lb = self.P["ltrbs_head.head.0.weight"], self.P["ltrbs_head.head.0.bias"]
+            b = conv2d(res["decoder_b"], lw, lb, False,
+                       self._cache.get("ltrbs", [lw], lambda: pack_conv(lw)))
+        return o, b
+
+    def forward_units(self, feats: torch.Tensor, unit_image: Sequence[int], unit_boxes,
+                      want_aux: bool = False):
+        """One matching_net forward per unit (image unit_image[u], exemplar
+        unit_boxes[u]).  Returns dict(o, b, f_tm_relu, f0, fp)."""
+        unit_image = [int(i) for i in unit_image]
+        fp, f0 = self.project(feats, want_f0=want_aux)
+        if self.cfg.no_matcher:
+            ui = torch.as_tensor(unit_image, device=fp.device, dtype=torch.long)
+            f_tm = fp.index_select(0, ui).contiguous()
+            relu = torch.relu(f_tm) if want_aux else None
+        else:
+            f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux)
+        o, b = self.decode(fp, f_tm, unit_image)
+        return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
+
+    # ------------------------------------------------------------ post
+    @staticmethod
+    def peaks(o: torch.Tensor, b: Optional[torch.Tensor], params: np.ndarray,
+              input_is_prob: bool = False):
+        """Peak finder + decode per unit -> (logits, box, ref, counts) with
+        per-unit stride H*W."""
+        require_gpu(o, "objectness")
+        o = o.float().contiguous()
+        U = o.shape[0]
+        H, W = o.shape[-2:]
+        dev = o.device
+        cap = H * W
+        prm = torch.from_numpy(params.view(np.uint8).copy()).to(dev)
+        prob = torch.empty((U, H, W), device=dev, dtype=torch.float32)
+        logits = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
+        box = torch.empty((U * cap, 4), device=dev, dtype=torch.float32)
+        ref = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
+        counts = torch.empty(U, device=dev, dtype=torch.int32)
+        bb = b.float().contiguous() if b is not None else None
+        call("tmr_peaks_decode", ptr(o), int(input_is_prob), ptr(bb) if bb is not None else None,
+             U, H, W, ptr(prm), ptr(prob), ptr(logits), ptr(box), ptr(ref), ptr(counts), stream())
+        return logits, box, ref, counts, prob
+
+    @staticmethod
+    def nms(logits, box, ref, counts: torch.Tensor, counts_host: np.ndarray,
+            unit_off: torch.Tensor, seg_units: np.ndarray, iou_threshold: float,
+            want_keep: bool = False):
+        """Greedy NMS per image over its units' candidates (+ dummy rows).
+        Returns per-image lists of (logits, boxes, refs) device tensors
+        (+ keep indices when want_keep)."""
+        dev = logits.device
+        G = len(seg_units) - 1
+        cand_off, mask_off, max_cand = host.nms_offsets(counts_host, seg_units)
+        T = int(cand_off[-1])
+        work = torch.empty(max(load().tmr_nms_work_size(T, int(mask_off[-1])), 1), device=dev,
+                           dtype=torch.uint8)
+        seg_d = torch.as_tensor(np.asarray(seg_units, np.int32), device=dev)
+        coff_d = torch.as_tensor(cand_off, device=dev)
+        moff_d = torch.as_tensor(mask_off, device=dev)
+        out_l = torch.empty((T, 2), device=dev, dtype=torch.float32)
+        out_b = torch.empty((T, 4), device=dev, dtype=torch.float32)
+        out_r = torch.empty((T, 2), device=dev, dtype=torch.float32)
+        kept = torch.empty(G, device=dev, dtype=torch.int32)
+        keep = torch.empty(T, device=dev, dtype=torch.int64) if want_keep else None
+        call("tmr_nms", ptr(logits), ptr(box), ptr(ref), ptr(counts), ptr(unit_off), ptr(seg_d),
+             ptr(coff_d), ptr(moff_d), G, T, max_cand, float(iou_threshold), ptr(out_l), ptr(out_b),
+             ptr(out_r), ptr(keep) if keep is not None else None, ptr(kept), ptr(work), stream())
+        k = kept.cpu().numpy()  # variable-length result: one sync
+        L, Bx, R, K = [], [], [], []
+        for g in range(G):
+            s, e = int(cand_off[g]), int(cand_off[g]) + int(k[g])
+            L.append(out_l[s:e]); Bx.append(out_b[s:e]); R.append(out_r[s:e])
+            if keep is not None:
+                K.append(keep[s:e])
+        return (L, Bx, R, K) if want_keep else (L, Bx, R)
+
+    def detect(self, feats: torch.Tensor, exemplars, cls_ths: float, iou_threshold: float,
+               ablation_b: bool = False, ablation_c: bool = False):
+        """The reference's multi-exemplar inference (demo.py:106-130,
+        trainer.py:95-118) for a batch: per image, one forward per exemplar,
+        Get_pred_boxes, concat in exemplar order, one NMS.
+
+        exemplars: [B,E,4] normalised xyxy (array or tensor).
+        Returns per-image lists (logits [k,2], boxes [k,4], refs [k,2])."""
+        ex = exemplars.detach().cpu().numpy() if isinstance(exemplars, torch.Tensor) else \
+            np.asarray(exemplars)
+        ex = ex.astype(np.float32)
+        B, E = ex.shape[:2]
+        unit_image = np.repeat(np.arange(B), E)
+        boxes = ex.reshape(B * E, 4)
+        r = self.forward_units(feats, unit_image, boxes)
+        o, b = r["o"], r["b"]
+        H, W = o.shape[-2:]
+        params = host.peak_params(boxes, H, W, cls_ths, self.cfg.box_reg, ablation_b, ablation_c)
+        logits, box, ref, counts, _ = self.peaks(o, b, params)
+        counts_host = counts.cpu().numpy()  # torch.where-style sync (TM_utils.py:254)
+        U = B * E
+        unit_off = torch.arange(U, device=o.device, dtype=torch.int64) * (H * W)
+        seg = np.arange(0, U + 1, E, dtype=np.int64)
+        return self.nms(logits, box, ref, counts, counts_host, unit_off, seg, iou_threshold)

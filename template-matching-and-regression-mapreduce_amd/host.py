@@ -1,0 +1,156 @@
+"""Host-side descriptors for the HIP kernels.
+
+The reference sizes templates and peak kernels with Python scalar math on 0-d
+fp32 tensors (models/template_matching.py:56-73, utils/TM_utils.py:236-252,
+363-377).  These helpers reproduce that arithmetic exactly in numpy fp32 and
+pack it into the tmr_unit_t / tmr_peak_param_t structs of include/tmr.h.
+"""
+from __future__ import annotations
+
+import math
+from typing import Sequence, Tuple
+
+import numpy as np
+
+from ._lib import PEAK_DTYPE, TEMPLATE_PROTOTYPE, TEMPLATE_ROI_ALIGN, UNIT_DTYPE
+
+f32 = np.float32
+
+TEMPLATE_TYPES = {"roi_align": TEMPLATE_ROI_ALIGN, "prototype": TEMPLATE_PROTOTYPE}
+
+
+def clamp01(v) -> np.float32:
+    """min(1., max(0., v)) with Python's min/max semantics
+    (template_matching.py:58-59, TM_utils.py:237-238)."""
+    v = f32(v)
+    m = v if v > f32(0.0) else f32(0.0)
+    return m if m < f32(1.0) else f32(1.0)
+
+
+def clamp_box(box) -> np.ndarray:
+    b = np.asarray(box, dtype=np.float32).reshape(4)
+    return np.array([clamp01(x) for x in b], np.float32)
+
+
+def template_size(box, H: int, W: int) -> Tuple[np.ndarray, int, int]:
+    """(roi in feature px, Ht, Wt) exactly as extract_template computes them
+    (template_matching.py:56-73).  Raises ValueError where the reference would
+    ask roi_align for a non-positive output size."""
+    c = clamp_box(box)
+    x1, x2 = f32(c[0] * f32(W)), f32(c[2] * f32(W))
+    y1, y2 = f32(c[1] * f32(H)), f32(c[3] * f32(H))
+    wt = math.ceil(float(x2)) - math.floor(float(x1))
+    ht = math.ceil(float(y2)) - math.floor(float(y1))
+    if wt % 2 == 0:
+        wt -= 1
+    if ht % 2 == 0:
+        ht -= 1
+    if ht <= 0 or wt <= 0:
+        raise ValueError(f"exemplar box {np.asarray(box).tolist()} gives a {ht}x{wt} template "
+                         "(the reference's roi_align call fails for it too)")
+    if ht > H or wt > W:
+        raise ValueError(f"template {ht}x{wt} larger than the {H}x{W} feature map")
+    return np.array([x1, y1, x2, y2], np.float32), ht, wt
+
+
+def prototype_box(box, H: int, W: int) -> np.ndarray:
+    """Integer-snapped box of extract_prototype (template_matching.py:44-50)."""
+    c = clamp_box(box)
+    x1, x2 = f32(c[0] * f32(W)), f32(c[2] * f32(W))
+    y1, y2 = f32(c[1] * f32(H)), f32(c[3] * f32(H))
+    b = np.array([math.floor(float(x1)), math.floor(float(y1)), math.ceil(float(x2)),
+                  math.ceil(float(y2))], np.int32)
+    if b[2] <= b[0] or b[3] <= b[1]:
+        raise ValueError(f"exemplar box {np.asarray(box).tolist()} selects an empty region")
+    return b
+
+
+def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int,
+                template_type: str = "roi_align"):
+    """tmr_unit_t array for U units.  Returns (units, template_floats, max_ht, max_wt)."""
+    boxes = np.asarray(boxes, np.float32).reshape(-1, 4)
+    U = boxes.shape[0]
+    ttype = TEMPLATE_TYPES[template_type]
+    units = np.zeros(U, UNIT_DTYPE)
+    off = 0
+    max_ht = max_wt = 1
+    for u in range(U):
+        units["image"][u] = int(images[u])
+        units["type"][u] = ttype
+        if ttype == TEMPLATE_ROI_ALIGN:
+            roi, ht, wt = template_size(boxes[u], H, W)
+            units["roi"][u] = roi
+        else:
+            units["pbox"][u] = prototype_box(boxes[u], H, W)
+            ht = wt = 1
+        units["ht"][u] = ht
+        units["wt"][u] = wt
+        units["tmpl_offset"][u] = off
+        off += C * ht * wt
+        max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
+    return units, off, max_ht, max_wt
+
+
+# adaptive_kernel_generater (TM_utils.py:363-377) as 9-bit masks, bit (dy+1)*3+(dx+1)
+KERNEL_FULL = 0b111111111
+KERNEL_CENTER = 1 << 4
+KERNEL_VERT = (1 << 1) | (1 << 4) | (1 << 7)
+KERNEL_HORZ = (1 << 3) | (1 << 4) | (1 << 5)
+KERNEL_CROSS = KERNEL_VERT | KERNEL_HORZ
+
+
+def adaptive_mask(ex_h, ex_w, H: int, W: int) -> int:
+    """ex_h/ex_w are fp32 (0-d tensor arithmetic); torch compares them with the
+    Python double k/H cast to fp32."""
+    ex_h, ex_w = f32(ex_h), f32(ex_w)
+    nh, nw = 1.0 / H, 1.0 / W
+    h3, w3, h2, w2 = f32(nh * 3), f32(nw * 3), f32(nh * 2), f32(nw * 2)
+    if ex_h >= h3 and ex_w >= w3:
+        return KERNEL_FULL
+    if ex_h < h2 and ex_w < w2:
+        return KERNEL_CENTER
+    if ex_h < h2 and ex_w >= w2:
+        return KERNEL_VERT
+    if ex_h >= h2 and ex_w < w2:
+        return KERNEL_HORZ
+    return KERNEL_CROSS
+
+
+def mask_to_kernel(mask: int):
+    """9-bit mask -> the 3x3 list adaptive_kernel_generater returns."""
+    return [[(mask >> (r * 3 + c)) & 1 for c in range(3)] for r in range(3)]
+
+
+def peak_params(boxes: np.ndarray, H: int, W: int, cls_ths: float, box_reg: bool = True,
+                ablation_b: bool = False, ablation_c: bool = False) -> np.ndarray:
+    """tmr_peak_param_t per unit (TM_utils.py:236-252, 264-276)."""
+    boxes = np.asarray(boxes, np.float32).reshape(-1, 4)
+    P = np.zeros(boxes.shape[0], PEAK_DTYPE)
+    thr = f32(cls_ths)
+    mode = 2 if not box_reg else (1 if ablation_c else 0)
+    for u, box in enumerate(boxes):
+        c = clamp_box(box)
+        bw, bh = f32(c[2] - c[0]), f32(c[3] - c[1])
+        P["thr"][u] = thr
+        P["scale_w"][u] = f32(1.0) if ablation_b else bw
+        P["scale_h"][u] = f32(1.0) if ablation_b else bh
+        P["mask"][u] = adaptive_mask(bh, bw, H, W)
+        P["mode"][u] = mode
+    return P
+
+
+def nms_offsets(counts: np.ndarray, seg_units: np.ndarray):
+    """Per-image candidate-union sizes (dummy row for an empty unit,
+    TM_utils.py:288-291) -> (cand_off[G+1], mask_off[G+1], max_cand)."""
+    counts = np.asarray(counts, np.int64)
+    G = len(seg_units) - 1
+    n = np.zeros(G, np.int64)
+    for g in range(G):
+        c = counts[seg_units[g]:seg_units[g + 1]]
+        n[g] = int(np.maximum(c, 1).sum())
+    cand_off = np.zeros(G + 1, np.int64)
+    cand_off[1:] = np.cumsum(n)
+    words = n * ((n + 63) // 64)
+    mask_off = np.zeros(G + 1, np.int64)
+    mask_off[1:] = np.cumsum(words)
+    return cand_off, mask_off, int(n.max()) if G else 0

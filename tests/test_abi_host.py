@@ -1,0 +1,158 @@
+"""CPU-only: the C-ABI library loads and exports every symbol include/tmr.h
+declares; host-side descriptor arithmetic matches the oracle bit for bit."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import tmr_amd
+from tmr_amd import _lib, host, synth
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "tmr.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(tmr_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    syms = header_symbols()
+    assert len(syms) >= 14
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes table out of sync with tmr.h"
+    L = tmr_amd.load()
+    assert L.tmr_version() == 1
+    assert L.tmr_strerror(0) == b"ok"
+    assert b"invalid" in L.tmr_strerror(-1)
+
+
+def test_struct_layouts():
+    assert _lib.UNIT_DTYPE.itemsize == 56
+    assert _lib.PEAK_DTYPE.itemsize == 24
+
+
+def test_size_queries_no_gpu():
+    L = tmr_amd.load()
+    assert L.tmr_conv_pack_size(2048, 1024, 3) == 16 * 128 * 9 * 8 * 128
+    assert L.tmr_conv_pack_size(512, 256, 1) == 4 * 8 * 32 * 128
+    assert L.tmr_conv_pack_size(10, 10, 4) == -1
+    assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 16 * 5 * 3 * 64
+    assert L.tmr_nms_work_size(10, 4) > 10 * 36
+
+
+def test_invalid_arguments_return_codes():
+    L = tmr_amd.load()
+    assert L.tmr_conv_pack(None, 1, 1, 3, None, None) == -1
+    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, 1, 1, 1, None, 0, None, None, None, None) == -1
+    assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0.5, *([None] * 7)) == -1
+
+
+def test_gpu_only_guard():
+    import torch
+    with pytest.raises(tmr_amd.TMRError):
+        tmr_amd.Decoder_model(8)(torch.zeros(1, 8, 4, 4))
+
+
+def _rand_boxes(seed, n):
+    u = synth.uniform(seed, 4 * n).reshape(n, 4).astype(np.float32)
+    x1 = u[:, 0] * 1.2 - 0.1
+    y1 = u[:, 1] * 1.2 - 0.1
+    return np.stack([x1, y1, x1 + 0.005 + u[:, 2] * 0.5, y1 + 0.005 + u[:, 3] * 0.5], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("HW", [(32, 32), (128, 128), (192, 192), (24, 40)])
+def test_template_sizing_matches_oracle(HW):
+    H, W = HW
+    for box in _rand_boxes(H * 7 + W, 400):
+        try:
+            roi, ht, wt = host.template_size(box, H, W)
+        except ValueError:
+            with pytest.raises(ValueError):
+                oracle.template_size(box, H, W)
+            continue
+        oroi, oht, owt = oracle.template_size(box, H, W)
+        assert (ht, wt) == (oht, owt)
+        assert np.array_equal(roi.view(np.uint32), oroi.view(np.uint32))
+        assert np.array_equal(host.prototype_box(box, H, W), oracle.prototype_box(box, H, W))
+
+
+def test_template_sizing_golden(golden):
+    g = golden("template")
+    H, W = g["f"].shape[-2:]
+    for i, box in enumerate(g["boxes"]):
+        roi, ht, wt = host.template_size(box, H, W)
+        assert (ht, wt) == tuple(g["sizes"][i])
+        assert np.array_equal(roi.view(np.uint32), g["rois"][i].view(np.uint32))
+
+
+def test_synthetic_boxes_give_requested_size():
+    for k in range(1, 32, 2):
+        for H in (64, 128, 192):
+            box = synth.exemplar_box(k, H, H, 5, 7)
+            _, ht, wt = host.template_size(box, H, H)
+            assert ht == k and wt == k
+
+
+@pytest.mark.parametrize("HW", [(128, 128), (24, 32), (192, 192)])
+def test_peak_params_match_oracle(HW):
+    H, W = HW
+    boxes = _rand_boxes(5, 300)
+    # include the exact kernel boundaries 2/H and 3/H
+    extra = np.array([[0.1, 0.1, 0.1 + 3.0 / W, 0.1 + 3.0 / H], [0.1, 0.1, 0.1 + 2.0 / W, 0.1 + 2.0 / H],
+                      [0.2, 0.2, 0.2 + 1.0 / W, 0.2 + 2.5 / H], [0, 0, 1, 1], [-1, -1, 0, 0]], np.float32)
+    boxes = np.concatenate([boxes, extra])
+    for ab_b in (False, True):
+        P = host.peak_params(boxes, H, W, 0.7, True, ab_b, False)
+        for u, box in enumerate(boxes):
+            s = oracle.exemplar_scalars(box, ab_b)
+            m = oracle.adaptive_kernel(s[0], s[1], H, W).reshape(9)
+            mask = sum(int(v) << i for i, v in enumerate(m))
+            assert P["mask"][u] == mask
+            assert P["scale_w"][u] == s[2] and P["scale_h"][u] == s[3]
+            assert P["thr"][u] == np.float32(0.7)
+
+
+def test_adaptive_kernel_api():
+    assert tmr_amd.adaptive_kernel_generater([0.5, 0.5], [128, 128]) == [[1, 1, 1]] * 3
+    assert tmr_amd.adaptive_kernel_generater([0.001, 0.001], [128, 128]) == [[0, 0, 0], [0, 1, 0], [0, 0, 0]]
+    assert tmr_amd.adaptive_kernel_generater([0.001, 0.5], [128, 128]) == [[0, 1, 0]] * 3
+    assert tmr_amd.adaptive_kernel_generater([0.5, 0.001], [128, 128]) == [[0, 0, 0], [1, 1, 1], [0, 0, 0]]
+    assert tmr_amd.adaptive_kernel_generater([2.5 / 128, 2.5 / 128], [128, 128]) == \
+        [[0, 1, 0], [1, 1, 1], [0, 1, 0]]
+
+
+def test_nms_offsets_dummy_rule():
+    counts = np.array([3, 0, 5, 0, 0, 2])
+    seg = np.array([0, 3, 6])
+    cand_off, mask_off, mx = host.nms_offsets(counts, seg)
+    assert cand_off.tolist() == [0, 9, 13]  # 3+1+5, 1+1+2
+    assert mx == 9
+    assert mask_off.tolist() == [0, 9, 13]  # n*ceil(n/64)
+
+
+def test_state_dict_keys_match_reference(golden):
+    from types import SimpleNamespace
+    import torch
+
+    class BB(torch.nn.Module):
+        num_channels = 16
+
+        def forward(self, x):
+            return x
+
+    for name in ["default", "squeeze", "nofusion", "noboxreg", "twolayer_k5", "nomatcher"]:
+        g = golden(f"forward_{name}")
+        import json
+        args = SimpleNamespace(**json.loads(str(g["args"])))
+        m = tmr_amd.matching_net(BB(), args)
+        ref_keys = sorted(k[3:] for k in g if k.startswith("sd."))
+        assert sorted(m.state_dict().keys()) == ref_keys, name
+        sd = {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd.")}
+        m.load_state_dict(sd, strict=True)

@@ -1,0 +1,330 @@
+"""GPU parity: libtmr.so (through the C ABI via the tmr_amd modules) against
+the golden vectors from the reference and the CPU oracle.
+
+Tolerances (written here):
+  fp32 maps (xcorr, decoder/heads, o/b): normwise max|d|/max|ref| <= 1e-5
+  templates (RoIAlign), upsample, peaks, keep indices, counts: bit-exact
+  box corners: bit-exact vs the oracle; vs the reference <= 2 ulp of the
+  row's largest |coordinate| (torch-CPU exp is position dependent)
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import tmr_amd
+from tmr_amd import host, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+DEV = torch.device("cuda:0")
+
+
+def normwise(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if a.size == 0:
+        return 0.0
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def corner_ok(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    if a.shape != b.shape:
+        return False
+    if a.size == 0:
+        return True
+    scale = np.spacing(np.abs(b).max(axis=-1, keepdims=True).astype(np.float32))
+    return bool((np.abs(a.astype(np.float64) - b) <= 2 * scale).all())
+
+
+def cuda(x):
+    return torch.as_tensor(x).to(DEV)
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# ----------------------------------------------------------------- templates
+def test_roi_align_bitexact_vs_oracle(golden):
+    g = golden("template")
+    f = cuda(g["f"])
+    m = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    mp = tmr_amd.TemplateMatching("prototype").to(DEV)
+    off = 0
+    for i, box in enumerate(g["boxes"]):
+        t = m.extract_template(f, torch.from_numpy(box)).cpu().numpy()[0]
+        ht, wt = g["sizes"][i]
+        assert t.shape == (f.shape[1], ht, wt)
+        ref = g["templates"][off:off + t.size].reshape(t.shape)
+        off += t.size
+        assert bits_equal(t, ref), i
+        p = mp.extract_prototype(f, torch.from_numpy(box)).cpu().numpy().ravel()
+        assert normwise(p, g["protos"][i]) <= TOL
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 128, 128), (32, 96, 96)])
+def test_roi_align_bitexact_large(C, H, W):
+    f = synth.normal(3, (1, C, H, W))
+    boxes = []
+    for k in (1, 3, 7, 15, 31):
+        boxes.append(synth.exemplar_box(k, H, W, 5, 9))
+    boxes.append(np.array([0.1, 0.2, 0.9, 0.95], np.float32))  # big template, sampling grid > 1
+    boxes.append(np.array([-0.2, 0.5, 0.3, 1.4], np.float32))  # clamped
+    m = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    fd = cuda(f)
+    for box in boxes:
+        roi, ht, wt = oracle.template_size(box, H, W)
+        ref = oracle.roi_align(f[0], roi, ht, wt)
+        got = m.extract_template(fd, torch.from_numpy(box)).cpu().numpy()[0]
+        assert bits_equal(got, ref)
+
+
+# ----------------------------------------------------------------- xcorr
+def test_xcorr_golden(golden):
+    g = golden("xcorr")
+    for i in range(int(g["n"])):
+        C, H, W, h, w, sq = g[f"c{i}_meta"].tolist()
+        f, t, ref = g[f"c{i}_f"], g[f"c{i}_t"], g[f"c{i}_out"]
+        # drive tmr_xcorr directly with the golden template (no RoIAlign)
+        units = np.zeros(1, tmr_amd._lib.UNIT_DTYPE)
+        units["ht"], units["wt"], units["tmpl_offset"] = h, w, 0
+        from tmr_amd._lib import call, ptr, stream
+        from tmr_amd.engine import _units_to_device
+        fd, td = cuda(f), cuda(t.reshape(-1))
+        out = torch.empty((1, 1 if sq else C, H, W), device=DEV)
+        relu = torch.empty_like(out)
+        work = torch.empty((1, C, H, W), device=DEV) if sq else None
+        scale = torch.ones(1, device=DEV)
+        ud = _units_to_device(units, DEV)
+        call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), 1, h, w, ptr(scale), sq, ptr(out),
+             ptr(relu), ptr(work) if work is not None else None, stream())
+        got = out.cpu().numpy()
+        assert normwise(got, ref) <= TOL, (i, normwise(got, ref))
+        assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0))
+        # the pad border is exactly zero
+        if h > 1:
+            assert (got[..., : h // 2, :] == 0).all() and (got[..., H - h // 2:, :] == 0).all()
+
+
+@pytest.mark.parametrize("k", [3, 9, 15, 31])
+def test_xcorr_large_vs_oracle(k):
+    C, H, W = 16, 128, 128
+    f = synth.normal(10 + k, (2, C, H, W))
+    boxes = np.stack([synth.exemplar_box(k, H, W, 3, 11), synth.exemplar_box(k, H, W, 40, 2)])
+    m = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    with torch.no_grad():
+        m.scale.fill_(0.75)
+    got = m(cuda(f), [torch.from_numpy(b[None]) for b in boxes]).cpu().numpy()
+    for b in range(2):
+        roi, ht, wt = oracle.template_size(boxes[b], H, W)
+        t = oracle.roi_align(f[b], roi, ht, wt)
+        ref = oracle.xcorr(f[b], t, 0.75)
+        assert normwise(got[b], ref) <= TOL
+
+
+# ----------------------------------------------------------------- convs
+@pytest.mark.parametrize("C,N,H,W,ks", [(64, 64, 32, 40, 3), (40, 72, 17, 33, 3), (16, 16, 24, 24, 5),
+                                        (24, 8, 20, 20, 1), (1024, 1024, 16, 32, 3), (12, 12, 9, 9, 7)])
+def test_decoder_conv_vs_torch(C, N, H, W, ks):
+    torch.manual_seed(C + N + ks)
+    x = torch.randn(2, C, H, W)
+    dec = tmr_amd.Decoder_model(C, 1, ks)
+    if N != C:
+        dec.layer[0] = torch.nn.Conv2d(C, N, ks, padding=ks // 2)
+    with torch.no_grad():
+        dec.layer[0].bias.normal_()
+    ref = torch.nn.functional.leaky_relu(dec.layer[0](x), 0.01).detach().numpy()
+    got = dec.to(DEV)(x.to(DEV)).cpu().numpy()
+    assert normwise(got, ref) <= TOL
+
+
+def test_heads_vs_torch():
+    torch.manual_seed(1)
+    x = torch.randn(3, 96, 20, 28)
+    for cls in (tmr_amd.ObjectnessHead, tmr_amd.BboxesHead):
+        h = cls(96)
+        with torch.no_grad():
+            h.head[0].bias.normal_()
+        ref = h.head[0](x).detach().numpy()
+        got = h.to(DEV)(x.to(DEV)).cpu().numpy()
+        assert normwise(got, ref) <= TOL
+
+
+# ----------------------------------------------------------------- forward
+class _Passthrough(torch.nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.num_channels = c
+
+    def forward(self, x):
+        return x
+
+
+@pytest.mark.parametrize("name", ["default", "squeeze", "prototype", "nofusion", "noboxreg",
+                                  "twolayer_k5", "noupsample", "nomatcher"])
+def test_matching_net_forward_golden(golden, name):
+    from types import SimpleNamespace
+    g = golden(f"forward_{name}")
+    args = SimpleNamespace(**json.loads(str(g["args"])))
+    model = tmr_amd.matching_net(_Passthrough(g["feats"].shape[1]), args)
+    sd = {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd.")}
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV).eval()
+    ex = [cuda(e) for e in g["exemplars"]]
+    os_, bs_, ftm, f0 = model(cuda(g["feats"]), ex)
+    assert normwise(os_[0].cpu().numpy(), g["o"]) <= TOL
+    if "b" in g:
+        assert normwise(bs_[0].cpu().numpy(), g["b"]) <= TOL
+    else:
+        assert bs_[0] is None
+    assert normwise(ftm[0].cpu().numpy(), g["f_tm"]) <= TOL
+    f0n = f0.cpu().numpy()
+    assert normwise(f0n, g["f0"]) <= 1e-6
+    if args.feature_upsample:  # the fma form is bit-exact with the C restatement
+        assert bits_equal(f0n, np.stack([oracle.upsample2x(x) for x in g["feats"]]))
+
+
+# ----------------------------------------------------------------- peaks
+def _split(g, key):
+    counts = g[key + "_counts"]
+    out, o = [], 0
+    for c in counts:
+        out.append(g[key][o:o + c]); o += c
+    return out
+
+
+def test_get_pred_boxes_golden(golden):
+    """Bit-exact given identical score maps: feed the reference's own
+    sigmoid output (input_is_prob) and compare every candidate."""
+    g = golden("pred_boxes")
+    for i in range(int(g["n"])):
+        meta = json.loads(str(g[f"c{i}_meta"]))
+        prob, reg, ex = g[f"c{i}_prob"], g[f"c{i}_reg"], g[f"c{i}_ex"]
+        batch = {"regression_ablation_b": meta["ab_b"], "regression_ablation_c": meta["ab_c"]}
+        exl = [cuda(e[None]) for e in ex]
+        regs = [cuda(reg)] if meta["box_reg"] else [None]
+        L, Bx, R = tmr_amd.Get_pred_boxes([cuda(prob[:, None])], regs, exl, batch, meta["thr"],
+                                          meta["box_reg"], input_is_prob=True)
+        gL, gB, gR = _split(g, f"c{i}_logits"), _split(g, f"c{i}_boxes"), _split(g, f"c{i}_refs")
+        oL, oB, oR = oracle.get_pred_boxes_prob(list(prob), list(reg) if meta["box_reg"] else None,
+                                                [e[None] for e in ex], meta["thr"], meta["box_reg"],
+                                                meta["ab_b"], meta["ab_c"])
+        for b in range(len(gL)):
+            l, bx, r = L[b].cpu().numpy(), Bx[b].cpu().numpy(), R[b].cpu().numpy()
+            assert bits_equal(l, gL[b]), (i, b, meta)
+            assert bits_equal(r, gR[b]), (i, b)
+            assert corner_ok(bx, gB[b]), (i, b)
+            assert bits_equal(bx, oB[b]), (i, b)  # same correctly rounded exp as the oracle
+
+
+def test_peaks_large_random_vs_oracle():
+    """128x128 maps with plateaus, saturation, every kernel shape; bit-exact."""
+    H = W = 128
+    o = synth.normal(77, (6, 1, H, W)) * 3.0
+    o[0, 0, 10:20, 10:20] = 2.0
+    o[1, 0, 50:52, :] = 30.0
+    reg = synth.normal(78, (6, 4, H, W)) * 0.5
+    boxes = np.array([[0.1, 0.1, 0.3, 0.3], [0.1, 0.1, 0.1 + 1 / 256, 0.1 + 1 / 256],
+                      [0.1, 0.1, 0.2, 0.1 + 1 / 256], [0.1, 0.1, 0.1 + 1 / 256, 0.2],
+                      [0.1, 0.1, 0.1 + 2.5 / 128, 0.1 + 2.5 / 128], [-0.1, 0.4, 0.2, 1.2]], np.float32)
+    prob = oracle.sigmoid_cr(o)
+    for thr in (0.1, 0.7):
+        batch = {"regression_ablation_b": False, "regression_ablation_c": False}
+        L, Bx, R = tmr_amd.Get_pred_boxes([cuda(o)], [cuda(reg)], [cuda(b[None]) for b in boxes],
+                                          batch, thr, True)
+        oL, oB, oR = oracle.get_pred_boxes_prob(list(prob[:, 0]), list(reg), [b[None] for b in boxes],
+                                                thr)
+        for b in range(6):
+            assert bits_equal(L[b].cpu().numpy(), oL[b]), (thr, b)
+            assert bits_equal(Bx[b].cpu().numpy(), oB[b]), (thr, b)
+            assert bits_equal(R[b].cpu().numpy(), oR[b]), (thr, b)
+
+
+# ----------------------------------------------------------------- nms
+def test_nms_golden(golden):
+    g = golden("nms")
+    for i in range(int(g["n"])):
+        bx, sc, thr = g[f"c{i}_boxes"], g[f"c{i}_scores"], float(g[f"c{i}_thr"])
+        keep = tmr_amd.NMS_process(cuda(bx), cuda(np.stack([sc, np.zeros_like(sc)], 1)), thr)
+        assert np.array_equal(keep.cpu().numpy(), g[f"c{i}_keep"]), i
+        if bx.shape[0]:
+            L, B, R = tmr_amd.NMS([cuda(np.stack([sc, np.zeros_like(sc)], 1))], [cuda(bx)],
+                                  [cuda(bx[:, :2].copy())], thr)
+            assert bits_equal(B[0].cpu().numpy(), g[f"c{i}_kept_boxes"]), i
+
+
+@pytest.mark.parametrize("n,thr", [(1, 0.5), (63, 0.5), (64, 0.15), (65, 0.5), (700, 0.5),
+                                   (3000, 0.5), (5000, 0.15)])
+def test_nms_random_vs_oracle(n, thr):
+    u = synth.uniform(n, 5 * n).reshape(n, 5).astype(np.float32)
+    xy = u[:, :2] * 0.9
+    bx = np.concatenate([xy, xy + 0.01 + u[:, 2:4] * 0.1], 1).astype(np.float32)
+    sc = (np.round(u[:, 4] * 64) / 64).astype(np.float32)  # ties
+    keep = tmr_amd.NMS_process(cuda(bx), cuda(np.stack([sc, np.zeros_like(sc)], 1)), thr)
+    assert np.array_equal(keep.cpu().numpy(), oracle.nms(bx, sc, thr))
+
+
+# ----------------------------------------------------------------- callers
+def test_caller_sequence_golden(golden):
+    """demo.Inference.infer / each_step_multi_exemplars through TMREngine.detect."""
+    g = golden("caller")
+    sd = {k[3:]: cuda(v) for k, v in g.items() if k.startswith("sd.")}
+    eng = tmr_amd.TMREngine(sd, tmr_amd.PathConfig(emb_dim=16))
+    for thr, iou in ((0.1, 0.5), (0.5, 0.15), (0.7, 0.5)):
+        L, Bx, R = eng.detect(cuda(g["feats"]), g["exemplars"], thr, iou)
+        tag = f"t{int(thr * 100)}_i{int(iou * 100)}"
+        gl, gb = g[f"{tag}_logits"], g[f"{tag}_boxes"]
+        assert L[0].shape == gl.shape, (tag, L[0].shape, gl.shape)
+        assert np.allclose(L[0].cpu().numpy(), gl, rtol=0, atol=1e-6)
+        assert np.allclose(Bx[0].cpu().numpy(), gb, rtol=1e-5, atol=1e-6)
+        assert bits_equal(R[0].cpu().numpy(), g[f"{tag}_refs"])
+
+
+def test_scripted_config_vs_oracle():
+    """Full scripted shapes (emb 512, SAM 256x64x64 -> 128x128, E=3): fp32
+    maps within 1e-5 of the torch-CPU oracle; then, given the GPU's own
+    probability maps, peaks and NMS bit-exact against the C oracle."""
+    B, E = 1, 3
+    P = oracle.reference_weights(0)
+    P["objectness_head.head.0.bias"] = torch.tensor([-1.0])
+    feats = synth.sam_features(5, B, 256, 64, 64)
+    ex, ks = synth.exemplar_set(6, B, E, 128, 128, 3, 15)
+    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig())
+    ui = np.repeat(np.arange(B), E)
+    r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
+    o, b = r["o"].cpu().numpy(), r["b"].cpu().numpy()
+    for u in range(B * E):
+        exm = [torch.from_numpy(ex.reshape(-1, 4)[u:u + 1])]
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]), exm, P)
+        assert normwise(o[u], ro[0][0].numpy()) <= TOL
+        assert normwise(b[u], rb[0][0].numpy()) <= TOL
+    params = host.peak_params(ex.reshape(-1, 4), 128, 128, 0.1)
+    logits, box, ref, counts, prob = tmr_amd.TMREngine.peaks(r["o"], r["b"], params)
+    prob_h = prob.cpu().numpy()
+    assert bits_equal(prob_h, oracle.sigmoid_cr(o[:, 0]))
+    counts_h = counts.cpu().numpy()
+    cands = []
+    for u in range(B * E):
+        _, lg, bx, rf = oracle.peaks_decode(prob_h[u], b[u], ex.reshape(-1, 4)[u], 0.1)
+        assert counts_h[u] == lg.shape[0]
+        s = u * 128 * 128
+        assert bits_equal(logits[s:s + counts_h[u]].cpu().numpy(), lg)
+        assert bits_equal(box[s:s + counts_h[u]].cpu().numpy(), bx)
+        cands.append((lg, bx, rf))
+    unit_off = torch.arange(B * E, device=DEV, dtype=torch.int64) * (128 * 128)
+    L, Bx, R = tmr_amd.TMREngine.nms(logits, box, ref, counts, counts_h, unit_off,
+                                      np.arange(0, B * E + 1, E), 0.5)
+    ol, ob, orf = oracle.nms_lists([np.concatenate([c[0] for c in cands])],
+                                   [np.concatenate([c[1] for c in cands])],
+                                   [np.concatenate([c[2] for c in cands])], 0.5)
+    assert bits_equal(L[0].cpu().numpy(), ol[0])
+    assert bits_equal(Bx[0].cpu().numpy(), ob[0])
+    assert bits_equal(R[0].cpu().numpy(), orf[0])
