@@ -1,0 +1,132 @@
+"""Data-parallel streaming driver: the MI355X replacement for the reference's
+Hadoop mapper/reducer (mapper.py:34-142, reducer.py:34-94).
+
+* Sharding replaces the mapper chunking: the global image (or tar-shard) list
+  is split into contiguous, count-balanced ranges, one process per GPU.
+* The reducer becomes one exchange step over RCCL (torch.distributed backend
+  "nccl" on ROCm; "gloo" in CPU tests): an all-gather of per-image counts and
+  of the kept detections (box 4 + score + ref 2), padded to the global max.
+* Rank 0 prints the reducer-style table per category (reducer.py:25-27,39-42)
+  with detection counts instead of the ONNX feature statistics.
+
+The per-rank compute is ``detect_fn(feats, exemplars) -> (logits, boxes, refs)``
+(TMREngine.detect on the GPU).  Only the tests inject another function.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROW = 7  # x1 y1 x2 y2 score ref_x ref_y
+
+
+def dist_env() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, count-balanced [start, end) of n items for this rank."""
+    q, r = divmod(n, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def category_of(shard_name: str) -> str:
+    """mapper.py:15-20."""
+    for c in ("Easy", "Normal", "Hard"):
+        if shard_name.startswith(c + "_"):
+            return c
+    return "Unknown"
+
+
+def pack_rows(logits: Sequence[torch.Tensor], boxes: Sequence[torch.Tensor],
+              refs: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-image kept detections -> (counts int32 [B], rows fp32 [sum k, 7])."""
+    dev = boxes[0].device if len(boxes) else torch.device("cpu")
+    counts = torch.tensor([int(b.shape[0]) for b in boxes], dtype=torch.int32, device=dev)
+    if len(boxes) == 0:
+        return counts, torch.zeros((0, ROW), device=dev)
+    rows = torch.cat([torch.cat([b.float(), l[:, :1].float(), r.float()], 1)
+                      for l, b, r in zip(logits, boxes, refs)], 0)
+    return counts, rows
+
+
+def all_gather_detections(counts: torch.Tensor, rows: torch.Tensor, group=None):
+    """The reducer's exchange step.  Every rank receives, in global image
+    order, the per-image counts and the concatenated detection rows.
+    Three all-gathers: image counts per rank, per-image counts (padded to the
+    largest rank), rows (padded to the largest rank total)."""
+    world = dist.get_world_size(group)
+    dev = rows.device
+    nimg = torch.tensor([counts.numel(), rows.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(nimg) for _ in range(world)]
+    dist.all_gather(sizes, nimg, group=group)
+    sizes = torch.stack(sizes).cpu().numpy()
+    bmax, rmax = int(sizes[:, 0].max()), int(sizes[:, 1].max())
+    cpad = torch.zeros(max(bmax, 1), dtype=torch.int32, device=dev)
+    cpad[:counts.numel()] = counts
+    call = [torch.zeros_like(cpad) for _ in range(world)]
+    dist.all_gather(call, cpad, group=group)
+    rpad = torch.zeros((max(rmax, 1), ROW), dtype=torch.float32, device=dev)
+    rpad[:rows.shape[0]] = rows
+    rall = [torch.zeros_like(rpad) for _ in range(world)]
+    dist.all_gather(rall, rpad, group=group)
+    g_counts = torch.cat([call[r][:int(sizes[r, 0])] for r in range(world)])
+    g_rows = torch.cat([rall[r][:int(sizes[r, 1])] for r in range(world)])
+    return g_counts, g_rows
+
+
+def split_rows(counts: torch.Tensor, rows: torch.Tensor) -> List[torch.Tensor]:
+    out, o = [], 0
+    for c in counts.tolist():
+        out.append(rows[o:o + c]); o += c
+    return out
+
+
+def reducer_table(categories: Sequence[str], counts: Sequence[int]) -> str:
+    """Per-category summary, in the reducer's table layout (reducer.py:25-27,39-42)."""
+    agg: Dict[str, List[int]] = {}
+    for c, n in zip(categories, counts):
+        agg.setdefault(c, []).append(int(n))
+    lines = [f"{'CATEGORY':<12} | {'IMAGES':>6} | {'DETECTIONS':>10} | {'AVG_DET':>8} | {'MAX_DET':>8}",
+             "-" * 70]
+    for c in sorted(agg):
+        v = agg[c]
+        lines.append(f"{c:<12} | {len(v):>6} | {sum(v):>10} | {sum(v) / len(v):>8.2f} | {max(v):>8}")
+    return "\n".join(lines)
+
+
+def run_sharded(detect_fn: Callable, feats_fn: Callable[[int, int], Tuple[torch.Tensor, np.ndarray]],
+                n_images: int, batch: int, rank: int, world: int, group=None):
+    """Process this rank's image range in batches; all-gather every batch's
+    detections.  feats_fn(start, end) -> (features [b,C,h,w], exemplars [b,E,4]).
+    Returns (global counts, global rows) of the last batch round and the list
+    of all global counts in image order."""
+    start, end = shard_range(n_images, rank, world)
+    mine = end - start
+    rounds = -(-max(shard_range(n_images, r, world)[1] - shard_range(n_images, r, world)[0]
+                    for r in range(world)) // batch)
+    all_counts = []
+    for k in range(rounds):
+        s = start + k * batch
+        e = min(s + batch, end)
+        if s < e:
+            feats, ex = feats_fn(s, e)
+            L, Bx, R = detect_fn(feats, ex)
+            counts, rows = pack_rows(L, Bx, R)
+        else:  # this rank ran out of images: contribute nothing
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+            counts = torch.zeros(0, dtype=torch.int32, device=dev)
+            rows = torch.zeros((0, ROW), device=dev)
+        if world > 1:
+            counts, rows = all_gather_detections(counts, rows, group)
+        all_counts.append(counts.cpu())
+    del mine
+    return torch.cat(all_counts) if all_counts else torch.zeros(0, dtype=torch.int32)

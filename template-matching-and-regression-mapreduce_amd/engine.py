@@ -114,6 +114,9 @@ class TMREngine:
         self.P = params
         self.cfg = cfg
         self._cache = _PackCache()
+        # when a list, decode() appends (start, end) torch.cuda.Events recorded
+        # on the launch stream around the fused decoder kernel (bench.py)
+        self.decoder_events = None
         if cfg.decoder_kernel_size not in (1, 3, 5, 7):
             raise TMRError("decoder_kernel_size must be 1, 3, 5 or 7")
 
@@ -216,9 +219,16 @@ class TMREngine:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
+            ev = None
+            if self.decoder_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             call("tmr_conv_heads", ptr(src0) if src0 is not None else None, C0, ptr(ui), ptr(f_tm),
                  C1, U, H, W, ptr(wp), ptr(bias), N, cfg.decoder_kernel_size, 1, ptr(hw), ptr(part),
                  stream())
+            if ev is not None:
+                ev[1].record()
+                self.decoder_events.append(ev)
             o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
             b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
             call("tmr_heads_reduce", ptr(part), N, U, H, W, ptr(hb), ptr(o),
