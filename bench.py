@@ -1,0 +1,178 @@
+"""bench.py -- images/sec of the TMR match+regress+NMS hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "config B"): per GPU a batch of 64
+synthetic SAM feature maps [64,256,64,64] fp32 (upsampled in-path to
+128x128), 3 exemplars per image with templates 3x3..15x15, reference-init
+weights (emb 512, fusion, 1-layer 3x3 decoders), cls 0.1 / IoU 0.5
+(scripts/train/TMR_FSCD147.sh:20-21).  One step = the whole path for the
+batch: upsample+proj, RoIAlign, xcorr, fused decoders+heads, peaks+decode,
+NMS over each image's exemplar union (+ for N>1 the RCCL all-gather of
+per-image counts and kept boxes that replaces the Hadoop reducer).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Prints one JSON line (rank 0).  `roofline` is the fused decoder kernel
+(tmr_conv_heads, >98% of the path's FLOPs) timed with HIP events on its
+launch stream; `cpu_baseline` is the CPU oracle (torch-CPU restatement of the
+reference forward + C peaks/NMS) on a bounded sample, rank 0, N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+from tmr_import import load_package  # noqa: E402
+
+tmr = load_package()
+from tmr_amd import driver, synth  # noqa: E402
+
+METRIC = "images/sec (whole node) match+regress+NMS; % HBM/MFMA roofline at 1/2/4/8 GPU"
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), spec
+H = W = 128               # matching map (64x64 SAM features upsampled x2)
+EMB, CIN, KS = 512, 256, 3
+
+
+def decoder_flops_per_unit() -> float:
+    """Algorithmic FLOPs of the two 3x3 1024->1024 decoders per (image,
+    exemplar) unit: 2 * H*W * N(=2048) * K(=1024*9)."""
+    return 2.0 * H * W * (2 * 2 * EMB) * (2 * EMB * KS * KS)
+
+
+def cpu_baseline(P, feats, ex, seconds: float):
+    """The reference forward on the host cores: torch-CPU restatement
+    (oracle/oracle.py, op for op the reference's ATen calls, one full forward
+    per exemplar like demo.py:111) + C peaks/NMS.  Bounded by `seconds`."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    Pc = {k: v.detach().cpu() for k, v in P.items()}
+    t0 = time.perf_counter()
+    n = 0
+    while n < feats.shape[0]:
+        f = torch.from_numpy(feats[n:n + 1])
+        Ls, Bs, Rs = [], [], []
+        for e in range(ex.shape[1]):
+            exm = [torch.from_numpy(ex[n, e:e + 1])]
+            with torch.no_grad():
+                o, b, _, _ = oracle.forward_torch(f, exm, Pc)
+            prob = o[0][0, 0].sigmoid().numpy()
+            l_, b_, r_ = oracle.get_pred_boxes_prob([prob], [b[0][0].numpy()], exm, 0.1)
+            Ls.append(l_[0]); Bs.append(b_[0]); Rs.append(r_[0])
+        oracle.nms_lists([np.concatenate(Ls)], [np.concatenate(Bs)], [np.concatenate(Rs)], 0.5)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} image(s) x {ex.shape[1]} exemplars of the same workload, "
+                      f"{dt:.1f} s, torch {torch.__version__} CPU ({threads} threads)"}
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the decoder kernel from the committed rocprofv3
+    PMC summary (profiles/), or None."""
+    p = os.path.join(REPO, "profiles", "decoder_pmc.json")
+    if os.path.exists(p):
+        with open(p) as fh:
+            return json.load(fh).get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--exemplars", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    rank, world, local = driver.dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    P = synth.reference_state_dict(0, device=dev)
+    eng = tmr.TMREngine(P, tmr.PathConfig())
+    B, E = a.batch, a.exemplars
+    feats = synth.sam_features(1000 + rank, B, CIN, H // 2, W // 2)
+    ex, _ = synth.exemplar_set(2000 + rank, B, E, H, W, 3, 15)
+    feats_d = torch.from_numpy(feats).to(dev)
+
+    def step():
+        L, Bx, R = eng.detect(feats_d, ex, cls_ths=0.1, iou_threshold=0.5)
+        if world > 1:
+            counts, rows = driver.pack_rows(L, Bx, R)
+            driver.all_gather_detections(counts, rows)
+        return L
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    eng.decoder_events = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        last = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dec_ms = [s.elapsed_time(e) for s, e in eng.decoder_events]
+    eng.decoder_events = None
+    kept = [int(x.shape[0]) for x in last]
+
+    if rank == 0:
+        ms_step = 1e3 * elapsed / a.steps
+        value = world * B / (elapsed / a.steps)
+        flops = decoder_flops_per_unit() * B * E
+        avg_s = float(np.mean(dec_ms)) / 1e3
+        achieved = flops / avg_s / 1e12
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (portable-PRNG SAM-like features, reference-init weights)",
+            "config": {"workload": "config B: 64x SAM feats 256x64x64 (->128x128), 3 exemplars, "
+                                   "templates 3x3-15x15, fp32, cls 0.1, IoU 0.5",
+                       "images_per_gpu": B, "exemplars": E, "feature": [CIN, H // 2, W // 2],
+                       "matching_map": [EMB, H, W], "parallelism": f"dp{world}",
+                       "mean_kept_per_image": round(float(np.mean(kept)), 1)},
+            "roofline": {"bound": "mfma", "kernel": "tmr_conv_heads (decoder_b+decoder_o+heads)",
+                         "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                         "traffic": load_traffic(), "avg_launch_ms": round(1e3 * avg_s, 3),
+                         "flops_per_launch": flops},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

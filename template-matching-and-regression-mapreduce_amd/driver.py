@@ -102,17 +102,31 @@ def reducer_table(categories: Sequence[str], counts: Sequence[int]) -> str:
     return "\n".join(lines)
 
 
+def round_image_ids(n_images: int, batch: int, world: int, k: int) -> List[int]:
+    """Global image ids gathered in round k, in rank order (the order
+    all_gather_detections returns them)."""
+    ids = []
+    for r in range(world):
+        s, e = shard_range(n_images, r, world)
+        ids.extend(range(min(s + k * batch, e), min(s + (k + 1) * batch, e)))
+    return ids
+
+
 def run_sharded(detect_fn: Callable, feats_fn: Callable[[int, int], Tuple[torch.Tensor, np.ndarray]],
                 n_images: int, batch: int, rank: int, world: int, group=None):
-    """Process this rank's image range in batches; all-gather every batch's
-    detections.  feats_fn(start, end) -> (features [b,C,h,w], exemplars [b,E,4]).
-    Returns (global counts, global rows) of the last batch round and the list
-    of all global counts in image order."""
+    """Process this rank's image range in batches of ``batch``; after every
+    round all-gather that round's detections.
+    feats_fn(start, end) -> (features [b,C,h,w], exemplars [b,E,4]).
+    Returns (counts [n_images] int32, rows per image) in global image order on
+    every rank (rows only for world == 1 or when gathered)."""
     start, end = shard_range(n_images, rank, world)
-    mine = end - start
-    rounds = -(-max(shard_range(n_images, r, world)[1] - shard_range(n_images, r, world)[0]
-                    for r in range(world)) // batch)
-    all_counts = []
+    longest = max(shard_range(n_images, r, world)[1] - shard_range(n_images, r, world)[0]
+                  for r in range(world))
+    rounds = -(-longest // batch)
+    counts_g = np.zeros(n_images, np.int32)
+    rows_g: List[torch.Tensor] = [None] * n_images
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cpu")
     for k in range(rounds):
         s = start + k * batch
         e = min(s + batch, end)
@@ -120,13 +134,14 @@ def run_sharded(detect_fn: Callable, feats_fn: Callable[[int, int], Tuple[torch.
             feats, ex = feats_fn(s, e)
             L, Bx, R = detect_fn(feats, ex)
             counts, rows = pack_rows(L, Bx, R)
-        else:  # this rank ran out of images: contribute nothing
-            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
-                else torch.device("cpu")
+        else:  # this rank ran out of images this round: contribute nothing
             counts = torch.zeros(0, dtype=torch.int32, device=dev)
             rows = torch.zeros((0, ROW), device=dev)
         if world > 1:
             counts, rows = all_gather_detections(counts, rows, group)
-        all_counts.append(counts.cpu())
-    del mine
-    return torch.cat(all_counts) if all_counts else torch.zeros(0, dtype=torch.int32)
+        ids = round_image_ids(n_images, batch, world, k)
+        per = split_rows(counts, rows)
+        for i, img in enumerate(ids):
+            counts_g[img] = int(counts[i])
+            rows_g[img] = per[i]
+    return counts_g, rows_g

@@ -74,3 +74,30 @@ def exemplar_set(seed: int, B: int, E: int, H: int, W: int, kmin: int = 3, kmax:
             ix = int(u[b, e, 2] * (W - k + 1))
             boxes[b, e] = exemplar_box(k, H, W, iy, ix)
     return boxes, ks
+
+
+def reference_state_dict(seed: int, cin: int = 256, emb: int = 512, num_layers: int = 1,
+                         k: int = 3, obj_bias: float = 0.0, device="cpu"):
+    """Random weights with the reference initialisation (regression_head.py:19-24:
+    N(0, 0.01) conv weights, zero bias; nn.Conv2d default for input_proj;
+    matcher.scale = 1.0), under the reference state_dict keys (fusion, box
+    regression).  ``obj_bias`` optionally shifts the objectness bias."""
+    import math
+
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    P = {"matcher.scale": torch.tensor([1.0])}
+    bound = 1.0 / math.sqrt(cin)
+    P["input_proj.0.weight"] = (torch.rand(emb, cin, 1, 1, generator=g) * 2 - 1) * bound
+    P["input_proj.0.bias"] = (torch.rand(emb, generator=g) * 2 - 1) * bound
+    d = 2 * emb
+    for pre in ("decoder_b", "decoder_o"):
+        for l in range(num_layers):
+            P[f"{pre}.layer.{2 * l}.weight"] = torch.randn(d, d, k, k, generator=g) * 0.01
+            P[f"{pre}.layer.{2 * l}.bias"] = torch.zeros(d)
+    P["objectness_head.head.0.weight"] = torch.randn(1, d, 1, 1, generator=g) * 0.01
+    P["objectness_head.head.0.bias"] = torch.full((1,), float(obj_bias))
+    P["ltrbs_head.head.0.weight"] = torch.randn(4, d, 1, 1, generator=g) * 0.01
+    P["ltrbs_head.head.0.bias"] = torch.zeros(4)
+    return {k_: v.float().to(device) for k_, v in P.items()}
