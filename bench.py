@@ -81,8 +81,9 @@ def cpu_baseline(P, feats, ex, seconds: float):
 
 
 def load_traffic():
-    """Per-launch HBM bytes of the decoder kernel from the committed rocprofv3
-    PMC summary (profiles/), or None."""
+    """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, raw) of the decoder
+    kernel from the committed rocprofv3 PMC summary of the current kernel
+    version (profiles/decoder_pmc.json), or None."""
     p = os.path.join(REPO, "profiles", "decoder_pmc.json")
     if os.path.exists(p):
         with open(p) as fh:
@@ -146,7 +147,7 @@ def main():
     if rank == 0:
         ms_step = 1e3 * elapsed / a.steps
         value = world * B / (elapsed / a.steps)
-        flops = decoder_flops_per_unit() * B * E
+        flops = eng.last_decoder_flops  # executed FLOPs of the timed launch
         avg_s = float(np.mean(dec_ms)) / 1e3
         achieved = flops / avg_s / 1e12
         out = {
@@ -163,7 +164,12 @@ def main():
                          "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                          "traffic": load_traffic(), "avg_launch_ms": round(1e3 * avg_s, 3),
-                         "flops_per_launch": flops},
+                         "flops_per_launch": flops,
+                         "flops_basis": "executed: the per-unit f_TM half (K=512*9) of the fused "
+                                        "decoder_b+decoder_o conv; the fp half (K=512*9) runs once "
+                                        "per image (tmr_conv_store) and is shared by its exemplars",
+                         "path_algorithmic_tflop_per_step": round(
+                             decoder_flops_per_unit() * B * E / 1e12, 2)},
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds)

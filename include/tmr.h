@@ -103,7 +103,11 @@ int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates
  * with bias and optional LeakyReLU(0.01) (regression_head.py:7-8), fp32 MFMA.
  * unit_image (device int32[U]) may be NULL (identity).
  * tmr_conv_store: out [U,N,H,W].
- * tmr_conv_heads: the fused decoder+1x1-head epilogue; out is never stored:
+ * tmr_conv_heads: the fused decoder+1x1-head epilogue; out is never stored.
+ *   acc_init (nullable, [img][N][H][W] indexed by unit_image) is added to the
+ *   accumulators before the K loop: with it the decoder's fp half
+ *   (conv over src0 = fp, computed once per image by tmr_conv_store) is shared
+ *   by the image's exemplars and only the f_TM half runs per unit:
  *   partials[t][j][u][h][w] += sum_{n in tile t} act(conv)[n] * headw[n][j], j<5
  *   (headw [ceil(N/128)*128][5] fp32, zero padded; j 0-3 = ltrbs_head,
  *   4 = objectness_head,
@@ -113,7 +117,8 @@ int tmr_conv_store(const float *src0, int C0, const int32_t *unit_image, const f
                    int ks, int leaky, float *out, void *stream);
 int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_image, const float *src1,
                    int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
-                   int ks, int leaky, const float *headw, float *partials, void *stream);
+                   int ks, int leaky, const float *headw, const float *acc_init,
+                   float *partials, void *stream);
 int64_t tmr_heads_partials_size(int N, int U, int H, int W);
 /* o [U,1,H,W] = head_bias[4] + sum_t partials[t][4];  b [U,4,H,W] (nullable) =
  * head_bias[j] + sum_t partials[t][j]. */

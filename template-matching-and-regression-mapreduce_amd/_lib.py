@@ -52,7 +52,7 @@ SIGNATURES = {
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
-    "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),
     "tmr_heads_reduce": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_peaks_decode": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),

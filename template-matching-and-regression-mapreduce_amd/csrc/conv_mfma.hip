@@ -53,6 +53,7 @@ struct ConvArgs {
     const float *wpack;
     const float *bias;
     const float *headw;
+    const float *acc_init;  // [img][N][H][W] added to the accumulators (nullable)
     float *out;
     float *partials;
     int C0, C1, U, H, W, N, NT, nchunks, MTX, MT;
@@ -110,11 +111,21 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_mfma_kernel(ConvArgs a) {
     const int wn = wave & 1, wm = wave >> 1;
     const int l32 = lane & 31, kh = lane >> 5;
 
-    int bid = blockIdx.x;
-    const int nt = bid % a.NT;
-    bid /= a.NT;
-    const int mt = bid % a.MT;
-    const int u = bid / a.MT;
+    // XCD-aware mapping: blocks b and b+8 share an XCD (round-robin dispatch),
+    // so the NT channel tiles of one (unit, pixel tile) are placed on the same
+    // XCD, back to back, and its input halo is fetched into that L2 once.
+    const int bid = blockIdx.x;
+    int nt, pos;
+    if (((a.MT * a.U) & 7) == 0) {
+        const int j = bid >> 3;
+        nt = j % a.NT;
+        pos = (j / a.NT) * 8 + (bid & 7);
+    } else {
+        nt = bid % a.NT;
+        pos = bid / a.NT;
+    }
+    const int mt = pos % a.MT;
+    const int u = pos / a.MT;
     const int y0 = (mt / a.MTX) * TH, x0 = (mt % a.MTX) * TW;
     const int img = a.unit_image ? a.unit_image[u] : u;
 
@@ -159,6 +170,23 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_mfma_kernel(ConvArgs a) {
     };
 
     f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+    if (a.acc_init) {
+        const int HWp = a.H * a.W;
+        const float *ai = a.acc_init + (size_t)img * a.N * HWp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int n0 = nt * BN + wn * 64 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+            const int ya = y0 + wm * 2, xa = x0 + l32;
+            const bool xin = xa < a.W;
+            auto ld = [&](int n, int y) -> float {
+                return (n < a.N && y < a.H && xin) ? ai[(size_t)n * HWp + (size_t)y * a.W + xa] : 0.0f;
+            };
+            acc00[r] = ld(n0, ya);
+            acc01[r] = ld(n0, ya + 1);
+            acc10[r] = ld(n0 + 32, ya);
+            acc11[r] = ld(n0 + 32, ya + 1);
+        }
+    }
 
     gload(0);
     lstore(0);
@@ -211,6 +239,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_mfma_kernel(ConvArgs a) {
             }
         }
     } else {
+        // stage this tile's head weights + bias (128 x 6 floats) in LDS so the
+        // unrolled reduction does not hoist 192 global loads into registers
+        float *hs = lds + 2048;  // [BN][8]: hw0..4, bias
+        for (int e = tid; e < BN * 6; e += NTHREADS) {
+            const int n = e / 6, q = e % 6, gn = nt * BN + n;
+            hs[n * 8 + q] = q < NHEAD ? a.headw[(size_t)gn * NHEAD + q] : (gn < a.N ? a.bias[gn] : 0.0f);
+        }
+        __syncthreads();
         float s[2][NHEAD];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
@@ -220,11 +256,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_mfma_kernel(ConvArgs a) {
         for (int ni = 0; ni < 2; ++ni) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int n = nbase + ni * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                const float bn = n < a.N ? a.bias[n] : 0.0f;
-                float hw[NHEAD];
-#pragma unroll
-                for (int j = 0; j < NHEAD; ++j) hw[j] = a.headw[(size_t)n * NHEAD + j];
+                const int nl = wn * 64 + ni * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const f32x4 h4 = *reinterpret_cast<const f32x4 *>(hs + nl * 8);
+                const float h5 = hs[nl * 8 + 4], bn = hs[nl * 8 + 5];
+                const float hw[NHEAD] = {h4[0], h4[1], h4[2], h4[3], h5};
 #pragma unroll
                 for (int mi = 0; mi < 2; ++mi) {
                     float v = accs[ni][mi][r] + bn;
@@ -410,8 +445,8 @@ extern "C" int tmr_upsample_proj(const float *feat, int B, int Cin, int Hin, int
 
 static int conv_common(const float *src0, int C0, const int32_t *unit_image, const float *src1,
                        int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
-                       int ks, int leaky, float *out, const float *headw, float *partials,
-                       int epi, void *stream) {
+                       int ks, int leaky, float *out, const float *headw, const float *acc_init,
+                       float *partials, int epi, void *stream) {
     TMR_REQUIRE(wpack && bias && U > 0 && H > 0 && W > 0 && N > 0 && C0 >= 0 && C1 >= 0);
     TMR_REQUIRE(C0 + C1 > 0 && (C0 == 0 || src0) && (C1 == 0 || src1) && ks_ok(ks));
     ConvArgs a = {};
@@ -428,6 +463,7 @@ static int conv_common(const float *src0, int C0, const int32_t *unit_image, con
     a.N = N;
     a.out = out;
     a.headw = headw;
+    a.acc_init = acc_init;
     a.partials = partials;
     a.leaky = leaky;
     return conv_dispatch(a, ks, false, epi, tmr_stream(stream));
@@ -439,16 +475,16 @@ extern "C" int tmr_conv_store(const float *src0, int C0, const int32_t *unit_ima
                               void *stream) {
     TMR_REQUIRE(out);
     return conv_common(src0, C0, unit_image, src1, C1, U, H, W, wpack, bias, N, ks, leaky, out,
-                       nullptr, nullptr, 0, stream);
+                       nullptr, nullptr, nullptr, 0, stream);
 }
 
 extern "C" int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_image,
                               const float *src1, int C1, int U, int H, int W, const float *wpack,
                               const float *bias, int N, int ks, int leaky, const float *headw,
-                              float *partials, void *stream) {
+                              const float *acc_init, float *partials, void *stream) {
     TMR_REQUIRE(headw && partials);
     return conv_common(src0, C0, unit_image, src1, C1, U, H, W, wpack, bias, N, ks, leaky,
-                       nullptr, headw, partials, 1, stream);
+                       nullptr, headw, acc_init, partials, 1, stream);
 }
 
 extern "C" int64_t tmr_heads_partials_size(int N, int U, int H, int W) {

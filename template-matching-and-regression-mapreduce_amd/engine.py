@@ -117,6 +117,12 @@ class TMREngine:
         # when a list, decode() appends (start, end) torch.cuda.Events recorded
         # on the launch stream around the fused decoder kernel (bench.py)
         self.decoder_events = None
+        # conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM): compute conv_fp once
+        # per image when several exemplars share it (fp32, changes only the
+        # summation order; same 1e-5 contract)
+        self.share_fp_half = True
+        self.last_decoder_flops = 0.0
+        self.last_shared_flops = 0.0
         if cfg.decoder_kernel_size not in (1, 3, 5, 7):
             raise TMRError("decoder_kernel_size must be 1, 3, 5 or 7")
 
@@ -132,9 +138,11 @@ class TMREngine:
         wp = self._cache.get("proj", [w], lambda: pack_conv(w))
         return wp, b.detach().float().contiguous(), w.shape[0], w.shape[1]
 
-    def _fused_decoders(self):
+    def _fused_decoders(self, split_c0: int = 0):
         """Layer-0 weights of decoder_b and decoder_o concatenated along N, with
-        the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders)."""
+        the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders).
+        split_c0 > 0 additionally packs the input-channel halves [:c0] / [c0:]
+        (conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM))."""
         cfg = self.cfg
         layers = ([self._dec_layers("decoder_b")[0]] if cfg.box_reg else []) + \
             [self._dec_layers("decoder_o")[0]]
@@ -161,9 +169,13 @@ class TMREngine:
             no = layers[-1][0].shape[0]
             hw[n0:n0 + no, 4] = ow.detach().float().reshape(no)
             hb[4] = ob.detach().float().reshape(())
-            return pack_conv(W), Bv, N, W.shape[1], hw.contiguous(), hb.contiguous()
+            split = None
+            if split_c0:
+                split = (pack_conv(W[:, :split_c0].contiguous()), pack_conv(W[:, split_c0:].contiguous()),
+                         torch.zeros(N, device=W.device, dtype=torch.float32))
+            return pack_conv(W), Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
 
-        return self._cache.get("fused_dec", tensors, build)
+        return self._cache.get(f"fused_dec{split_c0}", tensors, build)
 
     # ------------------------------------------------------------ forward
     def project(self, feats: torch.Tensor, want_f0: bool = False):
@@ -214,21 +226,38 @@ class TMREngine:
         ui = torch.as_tensor(np.asarray(unit_image, np.int32), device=dev)
         src0 = fp if cfg.fusion else None
         if cfg.decoder_num_layer == 1:
-            wp, bias, N, Cw, hw, hb = self._fused_decoders()
+            B = fp.shape[0]
+            # share the fp half of the decoder conv across an image's exemplars
+            # when that removes work (U >= 2B): conv_fp once per image, then
+            # the per-unit kernel starts from it and runs only the f_TM half
+            share = self.share_fp_half and cfg.fusion and U >= 2 * B
+            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0)
             if Cw != C0 + C1:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
+            acc0 = None
+            if share:
+                wp_fp, wp_tm, zero_b = split
+                acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
+                call("tmr_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp), ptr(zero_b),
+                     N, cfg.decoder_kernel_size, 0, ptr(acc0), stream())
+                wp, src0, C0k = wp_tm, None, 0
+            else:
+                C0k = C0
             ev = None
             if self.decoder_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            call("tmr_conv_heads", ptr(src0) if src0 is not None else None, C0, ptr(ui), ptr(f_tm),
-                 C1, U, H, W, ptr(wp), ptr(bias), N, cfg.decoder_kernel_size, 1, ptr(hw), ptr(part),
-                 stream())
+            call("tmr_conv_heads", ptr(src0) if src0 is not None else None, C0k, ptr(ui), ptr(f_tm),
+                 C1, U, H, W, ptr(wp), ptr(bias), N, cfg.decoder_kernel_size, 1, ptr(hw),
+                 ptr(acc0) if acc0 is not None else None, ptr(part), stream())
             if ev is not None:
                 ev[1].record()
                 self.decoder_events.append(ev)
+            self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * cfg.decoder_kernel_size ** 2 * U
+            self.last_shared_flops = (2.0 * H * W * N * C0 * cfg.decoder_kernel_size ** 2 * B
+                                      if share else 0.0)
             o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
             b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
             call("tmr_heads_reduce", ptr(part), N, U, H, W, ptr(hb), ptr(o),

@@ -288,6 +288,24 @@ def test_caller_sequence_golden(golden):
         assert bits_equal(R[0].cpu().numpy(), g[f"{tag}_refs"])
 
 
+def test_shared_fp_half_matches_unshared():
+    """conv(cat[fp,f_TM]) computed as conv_fp (once per image) + conv_tm (per
+    unit) agrees with the single fused conv within the fp32 contract."""
+    B, E = 2, 3
+    P = synth.reference_state_dict(3, cin=64, emb=128, obj_bias=-0.5)
+    feats = cuda(synth.sam_features(8, B, 64, 32, 32))
+    ex, _ = synth.exemplar_set(9, B, E, 64, 64, 3, 11)
+    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=128))
+    ui = np.repeat(np.arange(B), E)
+    r1 = eng.forward_units(feats, ui, ex.reshape(-1, 4))
+    assert eng.last_shared_flops > 0
+    eng.share_fp_half = False
+    r0 = eng.forward_units(feats, ui, ex.reshape(-1, 4))
+    assert eng.last_shared_flops == 0
+    assert normwise(r1["o"].cpu().numpy(), r0["o"].cpu().numpy()) <= TOL
+    assert normwise(r1["b"].cpu().numpy(), r0["b"].cpu().numpy()) <= TOL
+
+
 def test_scripted_config_vs_oracle():
     """Full scripted shapes (emb 512, SAM 256x64x64 -> 128x128, E=3): fp32
     maps within 1e-5 of the torch-CPU oracle; then, given the GPU's own
