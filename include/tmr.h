@@ -121,9 +121,26 @@ int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_image, const f
                    float *partials, void *stream);
 int64_t tmr_heads_partials_size(int N, int U, int H, int W);
 /* o [U,1,H,W] = head_bias[4] + sum_t partials[t][4];  b [U,4,H,W] (nullable) =
- * head_bias[j] + sum_t partials[t][j]. */
-int tmr_heads_reduce(const float *partials, int N, int U, int H, int W, const float *head_bias,
-                     float *o, float *b, void *stream);
+ * head_bias[j] + sum_t partials[t][j], t over ceil(N/tile_n) channel tiles
+ * (tile_n = 128 for tmr_conv_heads, 64 for tmr_wino_conv_heads). */
+int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int W,
+                     const float *head_bias, float *o, float *b, void *stream);
+
+/* ---- (a11) Winograd F(2x2,3x3) variant of the 3x3 decoder conv -------------
+ * Same semantics as tmr_conv_store / tmr_conv_heads for ks = 3 (pad 1), with
+ * 16 instead of 36 multiplies per 2x2 output tile (fp32 MFMA; fp32 transforms,
+ * same 1e-5 contract).  upack = U = G g G^T packed by tmr_wino_pack:
+ * [ceil(N/64)][ceil(C/8)][16 xi][2][64 n][4] fp32 (chunk channel c = 2*k4 + k2).  acc_init (nullable, [img][N][H][W])
+ * is added to the conv result before bias/activation in both variants. */
+int64_t tmr_wino_pack_size(int N, int C);
+int tmr_wino_pack(const float *w, int N, int C, float *upack, void *stream);
+int tmr_wino_conv_store(const float *src0, int C0, const int32_t *unit_image, const float *src1,
+                        int C1, int U, int H, int W, const float *upack, const float *bias, int N,
+                        int leaky, const float *acc_init, float *out, void *stream);
+int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, const float *src1,
+                        int C1, int U, int H, int W, const float *upack, const float *bias, int N,
+                        int leaky, const float *headw, const float *acc_init, float *partials,
+                        void *stream);
 
 /* ---- (a14-a16) peak finder + box decode ------------------------------------
  * Get_pred_boxes per unit (utils/TM_utils.py:245-282): p = sigmoid(o) (or o

@@ -54,7 +54,11 @@ SIGNATURES = {
     "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
     "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),
-    "tmr_heads_reduce": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "tmr_heads_reduce": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "tmr_wino_pack_size": (_L, [_I, _I]),
+    "tmr_wino_pack": (_I, [_P, _I, _I, _P, _P]),
+    "tmr_wino_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P]),
+    "tmr_wino_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "tmr_peaks_decode": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "tmr_nms_work_size": (_L, [_L, _L]),
     "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),

@@ -489,13 +489,14 @@ extern "C" int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_ima
 
 extern "C" int64_t tmr_heads_partials_size(int N, int U, int H, int W) {
     if (N <= 0 || U <= 0 || H <= 0 || W <= 0) return -1;
-    return tmr_cdiv(N, BN) * NHEAD * (int64_t)U * H * W;
+    return tmr_cdiv(N, 64) * NHEAD * (int64_t)U * H * W;  // enough for 64- and 128-wide tiles
 }
 
-extern "C" int tmr_heads_reduce(const float *partials, int N, int U, int H, int W,
+extern "C" int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int W,
                                 const float *head_bias, float *o, float *b, void *stream) {
     TMR_REQUIRE(partials && head_bias && o && N > 0 && U > 0 && H > 0 && W > 0);
-    int NT = (int)tmr_cdiv(N, BN);
+    TMR_REQUIRE(tile_n == 64 || tile_n == 128);
+    int NT = (int)tmr_cdiv(N, tile_n);
     int64_t tot = (int64_t)U * H * W;
     hipLaunchKernelGGL(heads_reduce_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0,
                        tmr_stream(stream), partials, NT, U, H * W, head_bias, o, b);

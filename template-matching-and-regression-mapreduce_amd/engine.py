@@ -88,6 +88,18 @@ def pack_conv(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pack_wino(w: torch.Tensor) -> torch.Tensor:
+    """[N,C,3,3] fp32 -> U = G g G^T in the tmr_wino_pack layout (include/tmr.h)."""
+    require_gpu(w, "conv weight")
+    w = w.detach().float().contiguous()
+    N, C, k1, k2 = w.shape
+    if (k1, k2) != (3, 3):
+        raise TMRError("Winograd F(2x2,3x3) needs 3x3 kernels")
+    out = torch.empty(load().tmr_wino_pack_size(N, C), device=w.device, dtype=torch.float32)
+    call("tmr_wino_pack", ptr(w), N, C, ptr(out), stream())
+    return out
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool, packed=None):
     """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the MFMA kernel."""
     require_gpu(x, "conv input")
@@ -121,8 +133,12 @@ class TMREngine:
         # per image when several exemplars share it (fp32, changes only the
         # summation order; same 1e-5 contract)
         self.share_fp_half = True
+        # 3x3 decoders: "wino" = Winograd F(2x2,3x3) kernel (16 instead of 36
+        # multiplies per 2x2 tile), "direct" = implicit GEMM over the 9 taps
+        self.decoder_algo = "wino" if cfg.decoder_kernel_size == 3 else "direct"
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
+        self.last_decoder_algo = None
         if cfg.decoder_kernel_size not in (1, 3, 5, 7):
             raise TMRError("decoder_kernel_size must be 1, 3, 5 or 7")
 
@@ -138,7 +154,7 @@ class TMREngine:
         wp = self._cache.get("proj", [w], lambda: pack_conv(w))
         return wp, b.detach().float().contiguous(), w.shape[0], w.shape[1]
 
-    def _fused_decoders(self, split_c0: int = 0):
+    def _fused_decoders(self, split_c0: int = 0, algo: str = "direct"):
         """Layer-0 weights of decoder_b and decoder_o concatenated along N, with
         the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders).
         split_c0 > 0 additionally packs the input-channel halves [:c0] / [c0:]
@@ -169,13 +185,15 @@ class TMREngine:
             no = layers[-1][0].shape[0]
             hw[n0:n0 + no, 4] = ow.detach().float().reshape(no)
             hb[4] = ob.detach().float().reshape(())
+            pk = pack_wino if algo == "wino" else pack_conv
             split = None
             if split_c0:
-                split = (pack_conv(W[:, :split_c0].contiguous()), pack_conv(W[:, split_c0:].contiguous()),
+                split = (pk(W[:, :split_c0].contiguous()), pk(W[:, split_c0:].contiguous()),
                          torch.zeros(N, device=W.device, dtype=torch.float32))
-            return pack_conv(W), Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
+            full = None if split_c0 else pk(W)
+            return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
 
-        return self._cache.get(f"fused_dec{split_c0}", tensors, build)
+        return self._cache.get(f"fused_dec{split_c0}_{algo}", tensors, build)
 
     # ------------------------------------------------------------ forward
     def project(self, feats: torch.Tensor, want_f0: bool = False):
@@ -231,36 +249,52 @@ class TMREngine:
             # when that removes work (U >= 2B): conv_fp once per image, then
             # the per-unit kernel starts from it and runs only the f_TM half
             share = self.share_fp_half and cfg.fusion and U >= 2 * B
-            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0)
+            algo = self.decoder_algo if cfg.decoder_kernel_size == 3 else "direct"
+            wino = algo == "wino"
+            ks = cfg.decoder_kernel_size
+            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0, algo)
             if Cw != C0 + C1:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
             acc0 = None
+            C0k = C0
             if share:
                 wp_fp, wp_tm, zero_b = split
                 acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
-                call("tmr_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp), ptr(zero_b),
-                     N, cfg.decoder_kernel_size, 0, ptr(acc0), stream())
+                if wino:
+                    call("tmr_wino_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
+                         ptr(zero_b), N, 0, None, ptr(acc0), stream())
+                else:
+                    call("tmr_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
+                         ptr(zero_b), N, ks, 0, ptr(acc0), stream())
                 wp, src0, C0k = wp_tm, None, 0
-            else:
-                C0k = C0
             ev = None
             if self.decoder_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            call("tmr_conv_heads", ptr(src0) if src0 is not None else None, C0k, ptr(ui), ptr(f_tm),
-                 C1, U, H, W, ptr(wp), ptr(bias), N, cfg.decoder_kernel_size, 1, ptr(hw),
-                 ptr(acc0) if acc0 is not None else None, ptr(part), stream())
+            s0 = ptr(src0) if src0 is not None else None
+            a0 = ptr(acc0) if acc0 is not None else None
+            if wino:
+                call("tmr_wino_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
+                     ptr(bias), N, 1, ptr(hw), a0, ptr(part), stream())
+            else:
+                call("tmr_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
+                     ptr(bias), N, ks, 1, ptr(hw), a0, ptr(part), stream())
             if ev is not None:
                 ev[1].record()
                 self.decoder_events.append(ev)
-            self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * cfg.decoder_kernel_size ** 2 * U
-            self.last_shared_flops = (2.0 * H * W * N * C0 * cfg.decoder_kernel_size ** 2 * B
-                                      if share else 0.0)
+            if wino:  # executed: 16 transform-domain GEMMs over 2x2 tiles
+                tiles = ((H + 1) // 2) * ((W + 1) // 2)
+                self.last_decoder_flops = 2.0 * 16 * tiles * N * (C0k + C1) * U
+                self.last_shared_flops = 2.0 * 16 * tiles * N * C0 * B if share else 0.0
+            else:
+                self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * ks ** 2 * U
+                self.last_shared_flops = 2.0 * H * W * N * C0 * ks ** 2 * B if share else 0.0
+            self.last_decoder_algo = algo
             o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
             b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
-            call("tmr_heads_reduce", ptr(part), N, U, H, W, ptr(hb), ptr(o),
+            call("tmr_heads_reduce", ptr(part), N, 64 if wino else 128, U, H, W, ptr(hb), ptr(o),
                  ptr(b) if b is not None else None, stream())
             return o, b
         # general depth: per-decoder conv stack, heads as 1x1 convs

@@ -43,7 +43,7 @@ def test_size_queries_no_gpu():
     assert L.tmr_conv_pack_size(2048, 1024, 3) == 16 * 128 * 9 * 8 * 128
     assert L.tmr_conv_pack_size(512, 256, 1) == 4 * 8 * 32 * 128
     assert L.tmr_conv_pack_size(10, 10, 4) == -1
-    assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 16 * 5 * 3 * 64
+    assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
     assert L.tmr_nms_work_size(10, 4) > 10 * 36
 
 

@@ -146,6 +146,50 @@ def test_decoder_conv_vs_torch(C, N, H, W, ks):
     assert normwise(got, ref) <= TOL
 
 
+@pytest.mark.parametrize("C,N,H,W,leaky", [(64, 64, 32, 40, True), (40, 72, 17, 33, True),
+                                           (13, 200, 9, 70, False), (1024, 256, 16, 32, True)])
+def test_wino_conv_vs_torch(C, N, H, W, leaky):
+    """Winograd F(2x2,3x3) kernel (tmr_wino_conv_store) vs ATen conv2d, incl.
+    odd sizes, channel counts off the 8/64 granules and an acc_init input."""
+    from tmr_amd._lib import call, ptr, stream
+    from tmr_amd.engine import pack_wino
+    torch.manual_seed(C * 7 + N)
+    x = torch.randn(2, C, H, W)
+    w = torch.randn(N, C, 3, 3) * (1.0 / (3 * C ** 0.5))
+    b = torch.randn(N)
+    init = torch.randn(2, N, H, W)
+    ref = torch.nn.functional.conv2d(x, w, b, padding=1) + init
+    if leaky:
+        ref = torch.nn.functional.leaky_relu(ref, 0.01)
+    out = torch.empty((2, N, H, W), device=DEV)
+    up = pack_wino(cuda(w))
+    xd, bd, initd = cuda(x), cuda(b), cuda(init)  # keep alive across the async launch
+    call("tmr_wino_conv_store", ptr(xd), C, None, None, 0, 2, H, W, ptr(up), ptr(bd), N,
+         int(leaky), ptr(initd), ptr(out), stream())
+    torch.cuda.synchronize()
+    assert normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
+def test_wino_matches_direct_decoders():
+    B, E = 2, 2
+    P = synth.reference_state_dict(4, cin=64, emb=96, obj_bias=-0.3)
+    feats = cuda(synth.sam_features(18, B, 64, 20, 23))
+    ex, _ = synth.exemplar_set(19, B, E, 40, 46, 3, 9)
+    ui = np.repeat(np.arange(B), E)
+    res = {}
+    for algo in ("wino", "direct"):
+        for share in (True, False):
+            eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=96))
+            eng.decoder_algo, eng.share_fp_half = algo, share
+            r = eng.forward_units(feats, ui, ex.reshape(-1, 4))
+            assert eng.last_decoder_algo == algo
+            res[(algo, share)] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
+    ref = res[("direct", False)]
+    for k, (o, b) in res.items():
+        assert normwise(o, ref[0]) <= TOL, k
+        assert normwise(b, ref[1]) <= TOL, k
+
+
 def test_heads_vs_torch():
     torch.manual_seed(1)
     x = torch.randn(3, 96, 20, 28)
