@@ -90,12 +90,16 @@ int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *
 /* ---- (a9+a4) depthwise cross-correlation + pad + scale -------------------
  * out[u] = pad(conv2d(f[img(u)], T_u, groups=C) / fl32(ht*wt)) * scale
  * (models/template_matching.py:23-41, :97).  scale is a device scalar.
+ * Units must be sorted by image; img_units (device int32[B+1]) gives each
+ * image's unit range, so the image's feature plane is staged once for all of
+ * its exemplars.
  * squeeze!=0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and
  * `work` must hold U*C*H*W floats; otherwise out is [U,C,H,W] and work may
  * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79). */
 int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
-              const tmr_unit_t *units, int U, int max_ht, int max_wt, const float *scale,
-              int squeeze, float *out, float *relu_out, float *work, void *stream);
+              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
+              const float *scale, int squeeze, float *out, float *relu_out, float *work,
+              void *stream);
 
 /* ---- (a10+a11+a12) conv stack ---------------------------------------------
  * Implicit-GEMM kxk conv over the virtual channel concat

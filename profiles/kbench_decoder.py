@@ -1,0 +1,82 @@
+"""Micro-benchmark of the decoder kernels at the config-B shape (128x128 maps,
+N = 2048 output channels, K = 512 input channels for the per-unit f_TM half):
+tmr_wino_conv_heads / tmr_conv_heads (and the *_store fp-half variants), HIP
+events on the launch stream, median of R repetitions.  Prints one JSON line.
+
+    python profiles/kbench_decoder.py [--units 48] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from tmr_import import load_package  # noqa: E402
+
+tmr = load_package()
+from tmr_amd._lib import call, load, ptr, stream  # noqa: E402
+from tmr_amd.engine import pack_conv, pack_wino  # noqa: E402
+
+FP32_PEAK = 157.3
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--units", type=int, default=48)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--H", type=int, default=128)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    U, H, W, C, N = a.units, a.H, a.H, 512, 2048
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = (torch.randn(U, C, H, W, generator=g) * 0.5).to(dev)
+    w = (torch.randn(N, C, 3, 3, generator=g) * 0.01).to(dev)
+    b = torch.zeros(N, device=dev)
+    hw = (torch.randn(N, 5, generator=g) * 0.01).to(dev)
+    acc0 = torch.randn(U, N, H, W, device=dev) * 0.1
+    part = torch.empty(load().tmr_heads_partials_size(N, U, H, W), device=dev)
+    uw, dw = pack_wino(w), pack_conv(w)
+    out = torch.empty(U, N, H, W, device=dev)
+    ui = torch.arange(U, device=dev, dtype=torch.int32)
+    res = {"units": U, "H": H, "K_channels": C, "N": N}
+    tiles = ((H + 1) // 2) * ((W + 1) // 2)
+    fl_w = 2.0 * 16 * tiles * N * C * U
+    fl_d = 2.0 * H * W * N * C * 9 * U
+    runs = {
+        "wino_heads": (lambda: call("tmr_wino_conv_heads", None, 0, ptr(ui), ptr(x), C, U, H, W, ptr(uw),
+                                    ptr(b), N, 1, ptr(hw), ptr(acc0), ptr(part), stream()), fl_w),
+        "wino_store": (lambda: call("tmr_wino_conv_store", ptr(x), C, None, None, 0, U, H, W, ptr(uw),
+                                    ptr(b), N, 0, None, ptr(out), stream()), fl_w),
+        "direct_heads": (lambda: call("tmr_conv_heads", None, 0, ptr(ui), ptr(x), C, U, H, W, ptr(dw),
+                                      ptr(b), N, 3, 1, ptr(hw), ptr(acc0), ptr(part), stream()), fl_d),
+    }
+    if os.environ.get("KB_ONLY"):
+        runs = {k: v for k, v in runs.items() if k in os.environ["KB_ONLY"].split(",")}
+    for name, (fn, fl) in runs.items():
+        fn()
+        torch.cuda.synchronize()
+        ms = timeit(fn, a.reps)
+        res[name] = {"ms": round(ms, 3), "executed_tflops": round(fl / ms / 1e9, 2),
+                     "frac_fp32_peak": round(fl / ms / 1e9 / FP32_PEAK, 4),
+                     "direct_equiv_tflops": round(fl_d / ms / 1e9, 2)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -14,12 +14,14 @@
 // Waves: 2 (xi halves) x 2 (32 channels) x 2 (32 tiles); a wave owns 8 xi x
 // 32x32 accumulators (128 VGPRs).  In the epilogue each wave applies its half
 // of A^T M A, the halves meet in LDS, and bias, LeakyReLU and the head
-// reduction run in registers.  Per 8-channel chunk each thread gathers one
-// (c, tile) 4x4 input window (unconditional loads from clamped addresses,
-// masked after), transforms it and writes its 16 V values to LDS; the U slab
-// is one contiguous float4 copy.  LDS images are [xi][k-half][row][4 k-steps]
-// so a lane's A (or B) operands for the chunk's 4 MFMA k-steps are one
-// ds_read_b128.  Double-buffered LDS (128 KB), one barrier per chunk.
+// reduction run in registers.  Pipeline per 8-channel chunk k (one barrier):
+// the U slab of chunk k+1 streams into LDS by LDS-DMA (the pack is the LDS
+// image), the zero-padded raw input halo of chunk k+2 is loaded coalesced
+// into registers, chunk k is computed, then each thread transforms one
+// (c, tile) 4x4 window of raw(k+1) from LDS into its 16 V values and stores
+// raw(k+2).  LDS images are [xi][k-half][row][4 k-steps] so a lane's A (or B)
+// operands for the chunk's 4 MFMA k-steps are one ds_read_b128.  LDS: V, U
+// and raw double buffered, 149 KB.
 #include "tmr_common.h"
 
 namespace {
@@ -37,9 +39,16 @@ constexpr int NHEAD = 5;
 constexpr int VS = 16 * CC * NTILE;  // floats, one V buffer  [16][2][64][4]
 constexpr int US = 16 * CC * BN;     // floats, one U buffer  [16][2][64][4]
 constexpr int US4 = US / 4;
-constexpr int UREG = US4 / NTHREADS;  // 4
+constexpr int UGLDS = US4 / NTHREADS;  // 4 LDS-DMA pieces (16 B/lane) per thread
+constexpr int HR = 2 * TR + 2, HC = 2 * TCOL + 2;  // raw input halo rows / cols
+constexpr int RS = CC * HR * HC;                   // floats, one raw buffer (2720)
+constexpr int RREG = (RS + NTHREADS - 1) / NTHREADS;
+constexpr int LDS_FLOATS = 2 * (VS + US + RS);
 static_assert(CC * NTILE == NTHREADS, "one (c, tile) window per thread");
 static_assert(US4 % NTHREADS == 0, "");
+static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS");
+
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
 
 struct WArgs {
     const float *src0;
@@ -67,8 +76,9 @@ __device__ __forceinline__ const float *chan_base(const WArgs &a, int img, int u
 template <int EPI>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_wino_kernel(WArgs a) {
     extern __shared__ float lds[];
-    float *Vs = lds;            // [2][16 xi][2 kh][64 tiles][4 ks]
-    float *Us = lds + 2 * VS;   // [2][16 xi][2 kh][64 n][4 ks]
+    float *Vs = lds;                 // [2][16 xi][2 kh][64 tiles][4 ks]
+    float *Us = lds + 2 * VS;        // [2][16 xi][2 kh][64 n][4 ks]
+    float *Rs = lds + 2 * (VS + US);  // [2][CC][HR][HC] raw input halo (zero padded)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -89,49 +99,65 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_wino_kernel(WArgs a) {
     const int ty0 = (mt / a.TX) * TR, tx0 = (mt % a.TX) * TCOL;
     const int img = a.unit_image ? a.unit_image[u] : u;
 
-    // this thread's (c, tile) input window; c = 2*ks + kh inside the chunk
-    const int wc = tid >> 6, wt = tid & 63;
-    const int wy = 2 * (ty0 + (wt >> 4)) - 1, wx = 2 * (tx0 + (wt & 15)) - 1;
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int y = wy + r, x = wx + s;
-            vmask |= (y >= 0 && y < a.H && x >= 0 && x < a.W ? 1u : 0u) << (r * 4 + s);
-        }
-    const int yc0 = wy < 0 ? 0 : wy, xc0 = wx < 0 ? 0 : wx;
-
+    // this thread's (c, tile) input window; c = 2*ks + kh inside the chunk.
+    // The map makes each half-wave's 32 V stores ((tile*4 + ks) dwords into
+    // the [kh][tile][ks] image) cover 8 tile residues x 4 ks = 32 banks.
+    const int wks = (lane >> 3) & 3, wkh = wave >> 2;
+    const int wt = (lane & 7) + 8 * ((wave & 3) * 2 + (lane >> 5));
+    const int wc = 2 * wks + wkh;
+    const int ctot = a.C0 + a.C1;
     const f32x4 *usrc = reinterpret_cast<const f32x4 *>(a.upack) + (size_t)nt * a.nchunks * US4;
-    f32x4 ureg[UREG];
-    float d[16];
-    int chv = 0;
 
-    auto gload = [&](int ch) {
-        const f32x4 *us = usrc + (size_t)ch * US4;
+    // raw halo elements this thread loads: chunk-invariant clamped offsets,
+    // channel-in-chunk and in-image bits (loads are unconditional; the value
+    // is zeroed on the way into LDS, never by a branch around the load)
+    int roff[RREG], rch[RREG];
+    uint32_t rok = 0;
 #pragma unroll
-        for (int i = 0; i < UREG; ++i) ureg[i] = us[tid + i * NTHREADS];
-        chv = ch * CC + wc;
-        const float *base = chan_base(a, img, u, chv);
+    for (int k = 0; k < RREG; ++k) {
+        const int e = tid + k * NTHREADS;
+        const int c = e / (HR * HC), rr = (e / HC) % HR, col = e % HC;
+        const int y = 2 * ty0 - 1 + rr, x = 2 * tx0 - 1 + col;
+        const bool ok = e < RS && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        roff[k] = min(max(y, 0), a.H - 1) * a.W + min(max(x, 0), a.W - 1);
+        rch[k] = e < RS ? c : 0;
+        rok |= (ok ? 1u : 0u) << k;
+    }
+    float xreg[RREG];
+    auto rload = [&](int ch) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int y = min(yc0 + (wy < 0 ? r - 1 : r), a.H - 1);
-            const float *row = base + (size_t)(y < 0 ? 0 : y) * a.W;
+        for (int k = 0; k < RREG; ++k) xreg[k] = chan_base(a, img, u, ch * CC + rch[k])[roff[k]];
+    };
+    auto rstore = [&](int ch, int buf) {
+        float *rd = Rs + buf * RS;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int x = min(xc0 + (wx < 0 ? s - 1 : s), a.W - 1);
-                d[r * 4 + s] = row[x < 0 ? 0 : x];
-            }
+        for (int k = 0; k < RREG; ++k) {
+            const int e = tid + k * NTHREADS;
+            if (RS % NTHREADS == 0 || e < RS)
+                rd[e] = (((rok >> k) & 1u) && ch * CC + rch[k] < ctot) ? xreg[k] : 0.0f;
         }
     };
-    auto lstore = [&](int buf) {
-        f32x4 *ud = reinterpret_cast<f32x4 *>(Us + buf * US);
+    auto uload = [&](int ch, int buf) {  // LDS-DMA: the pack is the LDS image
+        const f32x4 *us = usrc + (size_t)ch * US4;
+        float *ud = Us + buf * US;
 #pragma unroll
-        for (int i = 0; i < UREG; ++i) ud[tid + i * NTHREADS] = ureg[i];  // pack == LDS image
-        // zero the padding / out-of-range channel, then V = B^T d B
-        const uint32_t m = chv < a.C0 + a.C1 ? vmask : 0u;
+        for (int i = 0; i < UGLDS; ++i) {
+            const int piece = wave + i * (NTHREADS / 64);  // 1 KB pieces, wave-uniform base
+            __builtin_amdgcn_global_load_lds((const void *)(us + piece * 64 + lane),
+                                             (lds_ptr_t)(ud + piece * 256), 16, 0, 0);
+        }
+    };
+    // V = B^T d B of this thread's (c, tile) window, read from the raw image
+    const int wrow = 2 * (wt >> 4), wcol = 2 * (wt & 15);
+    auto transform = [&](int buf) {
+        const float *rs = Rs + buf * RS + wc * (HR * HC) + wrow * HC + wcol;
+        float d[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) d[q] = ((m >> q) & 1u) ? d[q] : 0.0f;
+        for (int r = 0; r < 4; ++r) {
+            const float2 p0 = *reinterpret_cast<const float2 *>(rs + r * HC);
+            const float2 p1 = *reinterpret_cast<const float2 *>(rs + r * HC + 2);
+            d[r * 4 + 0] = p0.x; d[r * 4 + 1] = p0.y; d[r * 4 + 2] = p1.x; d[r * 4 + 3] = p1.y;
+        }
         float t[16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -140,7 +166,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_wino_kernel(WArgs a) {
             t[r * 4 + 2] = d[r * 4 + 2] - d[r * 4 + 1];
             t[r * 4 + 3] = d[r * 4 + 1] - d[r * 4 + 3];
         }
-        float *vd = Vs + buf * VS + ((wc & 1) * NTILE + wt) * 4 + (wc >> 1);
+        float *vd = Vs + buf * VS + (wkh * NTILE + wt) * 4 + wks;
         constexpr int XS = 2 * NTILE * 4;  // floats per xi
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -157,14 +183,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_wino_kernel(WArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.0f;
 
-    gload(0);
-    lstore(0);
+    const int nch = a.nchunks;
+    // prologue: raw(0) + U(0) -> LDS; V(0) from raw(0), raw(1) -> LDS
+    rload(0);
+    uload(0, 0);
+    rstore(0, 0);
     __syncthreads();
-    for (int ch = 0; ch < a.nchunks; ++ch) {
-        const int buf = ch & 1;
-        if (ch + 1 < a.nchunks) gload(ch + 1);
-        const f32x4 *ub = reinterpret_cast<const f32x4 *>(Us + buf * US) + kh * 64 + wn * 32 + l32;
-        const f32x4 *vb = reinterpret_cast<const f32x4 *>(Vs + buf * VS) + kh * 64 + wtl * 32 + l32;
+    transform(0);
+    if (nch > 1) {
+        rload(1);
+        rstore(1, 1);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int cb = ch & 1, nb = cb ^ 1;
+        // ordinary loads first: hipcc drains vmcnt(0) before an ordinary load
+        // issued while an LDS-DMA is in flight
+        if (ch + 2 < nch) rload(ch + 2);
+        if (ch + 1 < nch) uload(ch + 1, nb);   // Us[nb] was last read by compute(ch-1)
+        const f32x4 *ub = reinterpret_cast<const f32x4 *>(Us + cb * US) + kh * 64 + wn * 32 + l32;
+        const f32x4 *vb = reinterpret_cast<const f32x4 *>(Vs + cb * VS) + kh * 64 + wtl * 32 + l32;
 #pragma unroll
         for (int x = 0; x < 8; ++x) {
             const int xi = wh * 8 + x;
@@ -174,8 +212,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_wino_kernel(WArgs a) {
             for (int ks = 0; ks < 4; ++ks)
                 acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[ks], b4[ks], acc[x], 0, 0, 0);
         }
-        if (ch + 1 < a.nchunks) lstore(buf ^ 1);
-        __syncthreads();
+        if (ch + 1 < nch) transform(nb);       // raw(ch+1) landed before the last barrier
+        if (ch + 2 < nch) rstore(ch + 2, cb);  // raw(ch) was consumed by the last transform
+        __syncthreads();                       // also drains the U LDS-DMA (vmcnt(0))
     }
 
     // ---------------- epilogue ----------------
@@ -306,7 +345,7 @@ __global__ void wino_pack_kernel(const float *__restrict__ w, int N, int C, int 
 
 template <int EPI>
 int launch_wino(WArgs a, hipStream_t s) {
-    const size_t lds = (size_t)2 * (VS + US) * sizeof(float);
+    const size_t lds = (size_t)LDS_FLOATS * sizeof(float);
     auto kern = conv_wino_kernel<EPI>;
     if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)

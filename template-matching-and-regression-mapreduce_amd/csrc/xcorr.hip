@@ -3,99 +3,151 @@
 // template area, the zero pad back to HxW and the learned scale:
 //   models/template_matching.py:23-41 (cross_correlation), :97 (f * scale).
 //
-// One workgroup per (band of 32 output rows, channel, unit).  The band's
-// input rows are staged once in LDS; each lane owns one output column and
-// RY=8 consecutive output rows and streams the input rows past them (register
-// sliding window), so each LDS read feeds RY*h/(RY+h-1) FMAs.  Template taps
-// are wave-uniform (scalar loads).  The divide is an IEEE fp32 division by
-// fl32(h*w) exactly like the reference's `/ (h*w + 1e-14)`.
+// One workgroup per (band of RB output rows, channel, image): the band's
+// input rows of the image's fp plane are staged once in LDS and reused by
+// every exemplar unit of that image (the reference's per-exemplar forwards
+// re-read it E times).  Each lane owns a 4x4 block of outputs and slides the
+// template over register windows (compile-time template width, wave-uniform
+// taps), ~11 FMAs per LDS read at 15x15.  The divide is an IEEE fp32 division
+// by fl32(h*w) exactly like the reference's `/ (h*w + 1e-14)`.
 #include "tmr_common.h"
 
 namespace {
 
 constexpr int NT = 256;
-constexpr int RY = 8;
-constexpr int JC = 8;
+constexpr int RY = 4;  // output rows per lane
+constexpr int RX = 4;  // output cols per lane
 
 struct XArgs {
     const float *f;
     const float *tmpl;
     const tmr_unit_t *units;
+    const int32_t *img_units;  // [B+1] unit ranges per image (units sorted by image)
     const float *scale;
     float *out;
     float *relu_out;
     float *work;
-    int C, H, W, RB, squeeze;
+    int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
 };
 
-__global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
-    extern __shared__ float xs[];
-    const int band = blockIdx.x, c = blockIdx.y, u = blockIdx.z;
-    const tmr_unit_t un = a.units[u];
-    const int h = un.ht, w = un.wt;
-    const int H = a.H, W = a.W;
-    const int ph = h / 2, pw = w / 2;
-    const int Ho = H - h + 1, Wo = W - w + 1;
-    const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
-    const int ya = max(yb0, ph), yz = min(yb1, ph + Ho);
-    const int nv = max(yz - ya, 0);
-    const float *__restrict__ fc = a.f + ((size_t)un.image * a.C + c) * H * W;
-    const float *__restrict__ tc = a.tmpl + un.tmpl_offset + (size_t)c * h * w;
-    const int nrows = nv ? nv + h - 1 : 0;
-    const int r_base = ya - ph;
-    for (int e = threadIdx.x; e < nrows * W; e += NT) xs[e] = fc[(size_t)r_base * W + e];
-    __syncthreads();
-
-    const float sc = a.squeeze ? 1.0f : *a.scale;
-    const float denom = (float)(h * w);
-    const size_t plane = (size_t)H * W;
-    float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                          : a.out + ((size_t)u * a.C + c) * plane;
-    float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
-
-    // zero border of this band (rows outside the valid range, cols outside)
-    if (!a.squeeze) {
-        for (int e = threadIdx.x; e < (yb1 - yb0) * W; e += NT) {
-            int yo = yb0 + e / W, xo = e % W;
-            bool valid = yo >= ya && yo < yz && xo >= pw && xo < pw + Wo;
-            if (!valid) {
-                op[(size_t)yo * W + xo] = 0.0f;
-                if (rp) rp[(size_t)yo * W + xo] = 0.0f;
+// acc[r][q] += sum_{i<h, j<KW} X[r0 + r + i][x0 + q + j] * T[i][j]
+template <int KW>
+__device__ __forceinline__ void corr_block(const float *xs, int W, int x0, int r0,
+                                           const float *__restrict__ tc, int h,
+                                           float (&acc)[RY][RX]) {
+    for (int ii = 0; ii < RY + h - 1; ++ii) {
+        const float *xr = xs + (r0 + ii) * W + x0;
+        float xv[KW + RX - 1];
+#pragma unroll
+        for (int j = 0; j < KW + RX - 1; ++j) xv[j] = xr[j];
+#pragma unroll
+        for (int r = 0; r < RY; ++r) {
+            const int i = ii - r;
+            if (i < 0 || i >= h) continue;  // wave-uniform
+            const float *tr = tc + i * KW;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const float t = tr[j];
+#pragma unroll
+                for (int q = 0; q < RX; ++q) acc[r][q] = fmaf(xv[q + j], t, acc[r][q]);
             }
         }
     }
+}
 
-    const int ngroups = (nv + RY - 1) / RY;
-    for (int task = threadIdx.x; task < Wo * ngroups; task += NT) {
-        const int x = task % Wo, r0 = (task / Wo) * RY;
-        float acc[RY];
+// generic width (templates wider than 31)
+__device__ __forceinline__ void corr_block_any(const float *xs, int W, int x0, int r0,
+                                               const float *__restrict__ tc, int h, int w,
+                                               float (&acc)[RY][RX]) {
+    for (int ii = 0; ii < RY + h - 1; ++ii) {
+        const float *xr = xs + (r0 + ii) * W + x0;
+        for (int r = 0; r < RY; ++r) {
+            const int i = ii - r;
+            if (i < 0 || i >= h) continue;
+            for (int j = 0; j < w; ++j) {
+                const float t = tc[i * w + j];
 #pragma unroll
-        for (int r = 0; r < RY; ++r) acc[r] = 0.0f;
-        for (int ii = 0; ii < RY + h - 1; ++ii) {
-            const float *xr = xs + (r0 + ii) * W + x;
-            for (int j0 = 0; j0 < w; j0 += JC) {
-                float xv[JC];
-#pragma unroll
-                for (int jj = 0; jj < JC; ++jj) xv[jj] = (j0 + jj < w) ? xr[j0 + jj] : 0.0f;
-#pragma unroll
-                for (int r = 0; r < RY; ++r) {
-                    const int i = ii - r;
-                    if (i < 0 || i >= h) continue;
-                    const float *tr = tc + i * w + j0;
-#pragma unroll
-                    for (int jj = 0; jj < JC; ++jj)
-                        if (j0 + jj < w) acc[r] = fmaf(xv[jj], tr[jj], acc[r]);
+                for (int q = 0; q < RX; ++q) acc[r][q] = fmaf(xr[q + j], t, acc[r][q]);
+            }
+        }
+    }
+}
+
+__device__ void corr_dispatch(int w, const float *xs, int W, int x0, int r0, const float *tc, int h,
+                              float (&acc)[RY][RX]) {
+    switch (w) {
+#define TMR_W(K) case K: corr_block<K>(xs, W, x0, r0, tc, h, acc); break;
+        TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
+        TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
+#undef TMR_W
+        default: corr_block_any(xs, W, x0, r0, tc, h, w, acc); break;
+    }
+}
+
+__global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
+    extern __shared__ float xs[];
+    const int band = blockIdx.x, c = blockIdx.y, img = blockIdx.z;
+    const int H = a.H, W = a.W;
+    const int u_beg = a.img_units[img], u_end = a.img_units[img + 1];
+    if (u_beg >= u_end) return;
+    const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
+    // input rows needed by any unit of this image: [yb0 - hmax/2, yb1 + hmax/2)
+    int hmax = 1;
+    for (int u = u_beg; u < u_end; ++u) hmax = max(hmax, a.units[u].ht);
+    const int rlo = max(yb0 - hmax / 2, 0), rhi = min(yb1 + hmax / 2, H);
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    const int nld = (rhi - rlo) * W;
+    for (int e = threadIdx.x; e < nld; e += NT) xs[e] = fc[(size_t)rlo * W + e];
+    // zero the slack rows/cols the 4x4 register blocks may over-read
+    for (int e = nld + threadIdx.x; e < a.LR * W + RX; e += NT) xs[e] = 0.0f;
+    __syncthreads();
+
+    const size_t plane = (size_t)H * W;
+    for (int u = u_beg; u < u_end; ++u) {
+        const tmr_unit_t un = a.units[u];
+        const int h = un.ht, w = un.wt;
+        const int ph = h / 2, pw = w / 2;
+        const int Ho = H - h + 1, Wo = W - w + 1;
+        const int ya = max(yb0, ph), yz = min(yb1, ph + Ho);  // valid output rows in band
+        const int nv = max(yz - ya, 0);
+        const float sc = a.squeeze ? 1.0f : *a.scale;
+        const float denom = (float)(h * w);
+        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
+                              : a.out + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        if (!a.squeeze) {  // zero border of this band
+            for (int e = threadIdx.x; e < (yb1 - yb0) * W; e += NT) {
+                const int yo = yb0 + e / W, xo = e % W;
+                if (!(yo >= ya && yo < yz && xo >= pw && xo < pw + Wo)) {
+                    op[(size_t)yo * W + xo] = 0.0f;
+                    if (rp) rp[(size_t)yo * W + xo] = 0.0f;
                 }
             }
         }
+        const float *__restrict__ tc = a.tmpl + un.tmpl_offset + (size_t)c * h * w;
+        const int nbx = (Wo + RX - 1) / RX, nby = (nv + RY - 1) / RY;
+        // LDS row of conv row (ya - ph): ya - ph - rlo
+        const int rbase = ya - ph - rlo;
+        for (int task = threadIdx.x; task < nbx * nby; task += NT) {
+            const int x0 = (task % nbx) * RX, r0 = (task / nbx) * RY;
+            float acc[RY][RX];
 #pragma unroll
-        for (int r = 0; r < RY; ++r) {
-            const int yl = r0 + r;
-            if (yl >= nv) break;
-            const size_t o = (size_t)(ya + yl) * W + x + pw;
-            const float v = (acc[r] / denom) * sc;
-            op[o] = v;
-            if (rp) rp[o] = v > 0.0f ? v : 0.0f;
+            for (int r = 0; r < RY; ++r)
+#pragma unroll
+                for (int q = 0; q < RX; ++q) acc[r][q] = 0.0f;
+            corr_dispatch(w, xs, W, x0, rbase + r0, tc, h, acc);
+#pragma unroll
+            for (int r = 0; r < RY; ++r) {
+                if (r0 + r >= nv) break;
+#pragma unroll
+                for (int q = 0; q < RX; ++q) {
+                    if (x0 + q >= Wo) break;
+                    const size_t o = (size_t)(ya + r0 + r) * W + x0 + q + pw;
+                    const float v = (acc[r][q] / denom) * sc;
+                    op[o] = v;
+                    if (rp) rp[o] = v > 0.0f ? v : 0.0f;
+                }
+            }
         }
     }
 }
@@ -125,19 +177,21 @@ __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_u
 }  // namespace
 
 extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
-                         const tmr_unit_t *units, int U, int max_ht, int max_wt,
-                         const float *scale, int squeeze, float *out, float *relu_out, float *work,
-                         void *stream) {
-    TMR_REQUIRE(f && templates && units && scale && out && B > 0 && C > 0 && U > 0);
+                         const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                         int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
+                         float *work, void *stream) {
+    TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
-    const int max_rows = (150 * 1024) / (4 * W);
+    // LDS rows: band + template halo + RY slack rows for partial 4-row blocks
+    const int max_rows = (150 * 1024) / (4 * W) - 1;
     const int RB = min(32, max_rows - (max_ht - 1) - RY);
     if (RB < 1) return TMR_E_UNSUPPORTED;
     XArgs a;
     a.f = f;
     a.tmpl = templates;
     a.units = units;
+    a.img_units = img_units;
     a.scale = scale;
     a.out = out;
     a.relu_out = relu_out;
@@ -147,14 +201,15 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     a.W = W;
     a.RB = RB;
     a.squeeze = squeeze;
-    const size_t lds = (size_t)(RB + max_ht - 1 + RY) * W * sizeof(float);
+    a.LR = RB + max_ht - 1 + RY;
+    const size_t lds = ((size_t)a.LR * W + RX) * sizeof(float);
     hipStream_t s = tmr_stream(stream);
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void *)xcorr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
         return TMR_E_HIP;
-    dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)U);
-    TMR_REQUIRE(C < 65536 && U < 65536);
+    TMR_REQUIRE(C < 65536 && B < 65536);
+    dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
     hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a);
     TMR_CHECK_LAUNCH();
     if (squeeze) {

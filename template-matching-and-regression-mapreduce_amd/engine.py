@@ -223,6 +223,8 @@ class TMREngine:
         units, tfl, mh, mw = host.build_units(unit_boxes, unit_image, H, W, C, cfg.template_type)
         dev = fp.device
         units_d = _units_to_device(units, dev)
+        img_units = host.image_ranges(unit_image, B)  # units are sorted by image
+        img_units_d = torch.as_tensor(img_units, device=dev)
         tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
         call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
         Co = 1 if cfg.squeeze else C
@@ -230,7 +232,8 @@ class TMREngine:
         relu = torch.empty_like(out) if want_relu else None
         work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
         scale = self.P["matcher.scale"].detach().float().contiguous()
-        call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), U, mh, mw, ptr(scale),
+        call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh, mw,
+             ptr(scale),
              int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
              ptr(work) if work is not None else None, stream())
         return out, relu

@@ -91,6 +91,16 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
     return units, off, max_ht, max_wt
 
 
+def image_ranges(unit_image: Sequence[int], B: int) -> np.ndarray:
+    """[B+1] int32 unit ranges per image; units must be sorted by image."""
+    ui = np.asarray(unit_image, np.int64)
+    if len(ui) and (np.any(np.diff(ui) < 0) or ui.min() < 0 or ui.max() >= B):
+        raise ValueError("units must be sorted by image and index images of the batch")
+    r = np.zeros(B + 1, np.int32)
+    r[1:] = np.cumsum(np.bincount(ui, minlength=B))
+    return r
+
+
 # adaptive_kernel_generater (TM_utils.py:363-377) as 9-bit masks, bit (dy+1)*3+(dx+1)
 KERNEL_FULL = 0b111111111
 KERNEL_CENTER = 1 << 4

@@ -50,7 +50,7 @@ def test_size_queries_no_gpu():
 def test_invalid_arguments_return_codes():
     L = tmr_amd.load()
     assert L.tmr_conv_pack(None, 1, 1, 3, None, None) == -1
-    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, 1, 1, 1, None, 0, None, None, None, None) == -1
+    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None) == -1
     assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0.5, *([None] * 7)) == -1
 
 

@@ -104,8 +104,10 @@ def test_xcorr_golden(golden):
         work = torch.empty((1, C, H, W), device=DEV) if sq else None
         scale = torch.ones(1, device=DEV)
         ud = _units_to_device(units, DEV)
-        call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), 1, h, w, ptr(scale), sq, ptr(out),
-             ptr(relu), ptr(work) if work is not None else None, stream())
+        iu = cuda(np.array([0, 1], np.int32))
+        call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), ptr(iu), 1, h, w, ptr(scale), sq,
+             ptr(out), ptr(relu), ptr(work) if work is not None else None, stream())
+        torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert normwise(got, ref) <= TOL, (i, normwise(got, ref))
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0))
