@@ -150,6 +150,17 @@ def main():
         flops = eng.last_decoder_flops  # executed FLOPs of the timed launch
         avg_s = float(np.mean(dec_ms)) / 1e3
         achieved = flops / avg_s / 1e12
+        # the per-unit f_TM half as a direct 3x3 conv: 2*H*W*N*(512*9) per unit
+        direct_equiv = 2.0 * H * W * (4 * EMB) * (EMB * KS * KS) * B * E
+        if eng.last_decoder_algo == "wino":
+            kernel_name = ("tmr_wino_conv_heads (Winograd F(2x2,3x3) decoder_b+decoder_o f_TM half "
+                           "+ LeakyReLU + 1x1 heads, fp32 MFMA 32x32x2)")
+            flops_basis = ("executed: 16 transform-domain GEMMs, 2*16*(H/2*W/2)*N(2048)*K(512) per "
+                           "unit; the fp half runs once per image (tmr_wino_conv_store) and is "
+                           "shared by its exemplars")
+        else:
+            kernel_name = "tmr_conv_heads (direct decoder_b+decoder_o f_TM half + heads)"
+            flops_basis = "executed: 2*H*W*N(2048)*K(512*9) per unit (f_TM half)"
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
@@ -160,14 +171,12 @@ def main():
                        "images_per_gpu": B, "exemplars": E, "feature": [CIN, H // 2, W // 2],
                        "matching_map": [EMB, H, W], "parallelism": f"dp{world}",
                        "mean_kept_per_image": round(float(np.mean(kept)), 1)},
-            "roofline": {"bound": "mfma", "kernel": "tmr_conv_heads (decoder_b+decoder_o+heads)",
+            "roofline": {"bound": "mfma", "kernel": kernel_name,
                          "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                          "traffic": load_traffic(), "avg_launch_ms": round(1e3 * avg_s, 3),
-                         "flops_per_launch": flops,
-                         "flops_basis": "executed: the per-unit f_TM half (K=512*9) of the fused "
-                                        "decoder_b+decoder_o conv; the fp half (K=512*9) runs once "
-                                        "per image (tmr_conv_store) and is shared by its exemplars",
+                         "flops_per_launch": flops, "flops_basis": flops_basis,
+                         "direct_conv_equivalent_tflops": round(direct_equiv / avg_s / 1e12, 2),
                          "path_algorithmic_tflop_per_step": round(
                              decoder_flops_per_unit() * B * E / 1e12, 2)},
         }
