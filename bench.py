@@ -38,8 +38,22 @@ from tmr_amd import driver, synth  # noqa: E402
 
 METRIC = "images/sec (whole node) match+regress+NMS; % HBM/MFMA roofline at 1/2/4/8 GPU"
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), spec
-H = W = 128               # matching map (64x64 SAM features upsampled x2)
 EMB, CIN, KS = 512, 256, 3
+
+# BASELINE.json configs; B is the metric's headline workload
+CONFIGS = {
+    "B": dict(desc="config B: 64x SAM feats 256x64x64 (->128x128), 3 exemplars, templates 3x3-15x15, "
+                   "fp32, cls 0.1, IoU 0.5", batch=64, E=3, hf=64, kmin=3, kmax=15, cls=0.1, iou=0.5),
+    "A": dict(desc="config A (demo.py shape): 1 image, SAM feats 256x64x64, 3 exemplars (k 7/11/15), "
+                   "fp32, cls 0.7, IoU 0.5", batch=1, E=3, hf=64, kmin=7, kmax=15, cls=0.7, iou=0.5),
+    "D": dict(desc="config D (RPINE streaming shape): 64x SAM feats 256x64x64, 1 exemplar, "
+                   "templates 3x3-15x15, fp32, cls 0.4, IoU 0.5", batch=64, E=1, hf=64, kmin=3,
+              kmax=15, cls=0.4, iou=0.5),
+    "E": dict(desc="config E (large-pattern stress): 8x SAM feats 256x96x96 (->192x192), 16 exemplars, "
+                   "templates 3x3-31x31, fp32, cls 0.1, IoU 0.5", batch=8, E=16, hf=96, kmin=3, kmax=31,
+              cls=0.1, iou=0.5),
+}
+H = W = 128  # set from the config in main()
 
 
 def decoder_flops_per_unit() -> float:
@@ -48,7 +62,7 @@ def decoder_flops_per_unit() -> float:
     return 2.0 * H * W * (2 * 2 * EMB) * (2 * EMB * KS * KS)
 
 
-def cpu_baseline(P, feats, ex, seconds: float):
+def cpu_baseline(P, feats, ex, seconds: float, cls: float, iou: float):
     """The reference forward on the host cores: torch-CPU restatement
     (oracle/oracle.py, op for op the reference's ATen calls, one full forward
     per exemplar like demo.py:111) + C peaks/NMS.  Bounded by `seconds`."""
@@ -68,9 +82,9 @@ def cpu_baseline(P, feats, ex, seconds: float):
             with torch.no_grad():
                 o, b, _, _ = oracle.forward_torch(f, exm, Pc)
             prob = o[0][0, 0].sigmoid().numpy()
-            l_, b_, r_ = oracle.get_pred_boxes_prob([prob], [b[0][0].numpy()], exm, 0.1)
+            l_, b_, r_ = oracle.get_pred_boxes_prob([prob], [b[0][0].numpy()], exm, cls)
             Ls.append(l_[0]); Bs.append(b_[0]); Rs.append(r_[0])
-        oracle.nms_lists([np.concatenate(Ls)], [np.concatenate(Bs)], [np.concatenate(Rs)], 0.5)
+        oracle.nms_lists([np.concatenate(Ls)], [np.concatenate(Bs)], [np.concatenate(Rs)], iou)
         n += 1
         if time.perf_counter() - t0 >= seconds:
             break
@@ -96,8 +110,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
-    ap.add_argument("--exemplars", type=int, default=3)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU per step")
+    ap.add_argument("--exemplars", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
@@ -108,15 +123,19 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    global H, W
+    cfg = CONFIGS[a.config]
+    H = W = 2 * cfg["hf"]
     P = synth.reference_state_dict(0, device=dev)
     eng = tmr.TMREngine(P, tmr.PathConfig())
-    B, E = a.batch, a.exemplars
+    B = a.batch or cfg["batch"]
+    E = a.exemplars or cfg["E"]
     feats = synth.sam_features(1000 + rank, B, CIN, H // 2, W // 2)
-    ex, _ = synth.exemplar_set(2000 + rank, B, E, H, W, 3, 15)
+    ex, _ = synth.exemplar_set(2000 + rank, B, E, H, W, cfg["kmin"], cfg["kmax"])
     feats_d = torch.from_numpy(feats).to(dev)
 
     def step():
-        L, Bx, R = eng.detect(feats_d, ex, cls_ths=0.1, iou_threshold=0.5)
+        L, Bx, R = eng.detect(feats_d, ex, cls_ths=cfg["cls"], iou_threshold=cfg["iou"])
         if world > 1:
             counts, rows = driver.pack_rows(L, Bx, R)
             driver.all_gather_detections(counts, rows)
@@ -152,12 +171,14 @@ def main():
         achieved = flops / avg_s / 1e12
         # the per-unit f_TM half as a direct 3x3 conv: 2*H*W*N*(512*9) per unit
         direct_equiv = 2.0 * H * W * (4 * EMB) * (EMB * KS * KS) * B * E
+        if eng.last_shared_flops == 0.0:  # unshared (E == 1): the launch covers both halves
+            direct_equiv *= 2
         if eng.last_decoder_algo == "wino":
             kernel_name = ("tmr_wino_conv_heads (Winograd F(2x2,3x3) decoder_b+decoder_o f_TM half "
                            "+ LeakyReLU + 1x1 heads, fp32 MFMA 32x32x2)")
-            flops_basis = ("executed: 16 transform-domain GEMMs, 2*16*(H/2*W/2)*N(2048)*K(512) per "
-                           "unit; the fp half runs once per image (tmr_wino_conv_store) and is "
-                           "shared by its exemplars")
+            flops_basis = ("executed: 16 transform-domain GEMMs, 2*16*(H/2*W/2)*N(2048)*K per unit "
+                           "(K=512: the fp half runs once per image in tmr_wino_conv_store and is "
+                           "shared by its exemplars; K=1024 when E=1)")
         else:
             kernel_name = "tmr_conv_heads (direct decoder_b+decoder_o f_TM half + heads)"
             flops_basis = "executed: 2*H*W*N(2048)*K(512*9) per unit (f_TM half)"
@@ -166,8 +187,7 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (portable-PRNG SAM-like features, reference-init weights)",
-            "config": {"workload": "config B: 64x SAM feats 256x64x64 (->128x128), 3 exemplars, "
-                                   "templates 3x3-15x15, fp32, cls 0.1, IoU 0.5",
+            "config": {"workload": cfg["desc"], "config": a.config,
                        "images_per_gpu": B, "exemplars": E, "feature": [CIN, H // 2, W // 2],
                        "matching_map": [EMB, H, W], "parallelism": f"dp{world}",
                        "mean_kept_per_image": round(float(np.mean(kept)), 1)},
@@ -181,7 +201,7 @@ def main():
                              decoder_flops_per_unit() * B * E / 1e12, 2)},
         }
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds, cfg["cls"], cfg["iou"])
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -352,15 +352,19 @@ def test_shared_fp_half_matches_unshared():
     assert normwise(r1["b"].cpu().numpy(), r0["b"].cpu().numpy()) <= TOL
 
 
-def test_scripted_config_vs_oracle():
-    """Full scripted shapes (emb 512, SAM 256x64x64 -> 128x128, E=3): fp32
+@pytest.mark.parametrize("hf,E,kmin,kmax,thr,iou", [(64, 3, 3, 15, 0.1, 0.5),    # config B shape
+                                                     (96, 3, 17, 31, 0.25, 0.5),  # config E shape (192^2)
+                                                     (64, 1, 5, 9, 0.4, 0.5)])    # config D (RPINE, E=1)
+def test_scripted_config_vs_oracle(hf, E, kmin, kmax, thr, iou):
+    """Full scripted shapes (emb 512, SAM 256 x hf x hf -> 2hf x 2hf maps): fp32
     maps within 1e-5 of the torch-CPU oracle; then, given the GPU's own
     probability maps, peaks and NMS bit-exact against the C oracle."""
-    B, E = 1, 3
+    B = 1
+    Hm = 2 * hf
     P = oracle.reference_weights(0)
     P["objectness_head.head.0.bias"] = torch.tensor([-1.0])
-    feats = synth.sam_features(5, B, 256, 64, 64)
-    ex, ks = synth.exemplar_set(6, B, E, 128, 128, 3, 15)
+    feats = synth.sam_features(5, B, 256, hf, hf)
+    ex, ks = synth.exemplar_set(6 + hf, B, E, Hm, Hm, kmin, kmax)
     eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig())
     ui = np.repeat(np.arange(B), E)
     r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
@@ -370,25 +374,51 @@ def test_scripted_config_vs_oracle():
         ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]), exm, P)
         assert normwise(o[u], ro[0][0].numpy()) <= TOL
         assert normwise(b[u], rb[0][0].numpy()) <= TOL
-    params = host.peak_params(ex.reshape(-1, 4), 128, 128, 0.1)
+    params = host.peak_params(ex.reshape(-1, 4), Hm, Hm, thr)
     logits, box, ref, counts, prob = tmr_amd.TMREngine.peaks(r["o"], r["b"], params)
     prob_h = prob.cpu().numpy()
     assert bits_equal(prob_h, oracle.sigmoid_cr(o[:, 0]))
     counts_h = counts.cpu().numpy()
     cands = []
     for u in range(B * E):
-        _, lg, bx, rf = oracle.peaks_decode(prob_h[u], b[u], ex.reshape(-1, 4)[u], 0.1)
+        _, lg, bx, rf = oracle.peaks_decode(prob_h[u], b[u], ex.reshape(-1, 4)[u], thr)
         assert counts_h[u] == lg.shape[0]
-        s = u * 128 * 128
+        s = u * Hm * Hm
         assert bits_equal(logits[s:s + counts_h[u]].cpu().numpy(), lg)
         assert bits_equal(box[s:s + counts_h[u]].cpu().numpy(), bx)
-        cands.append((lg, bx, rf))
-    unit_off = torch.arange(B * E, device=DEV, dtype=torch.int64) * (128 * 128)
+        cands.append((lg, bx, rf) if lg.shape[0] else (oracle.DUMMY_LOGITS, oracle.DUMMY_BOXES,
+                                                        oracle.DUMMY_REFS))
+    unit_off = torch.arange(B * E, device=DEV, dtype=torch.int64) * (Hm * Hm)
     L, Bx, R = tmr_amd.TMREngine.nms(logits, box, ref, counts, counts_h, unit_off,
-                                      np.arange(0, B * E + 1, E), 0.5)
+                                      np.arange(0, B * E + 1, E), iou)
     ol, ob, orf = oracle.nms_lists([np.concatenate([c[0] for c in cands])],
                                    [np.concatenate([c[1] for c in cands])],
-                                   [np.concatenate([c[2] for c in cands])], 0.5)
+                                   [np.concatenate([c[2] for c in cands])], iou)
     assert bits_equal(L[0].cpu().numpy(), ol[0])
     assert bits_equal(Bx[0].cpu().numpy(), ob[0])
     assert bits_equal(R[0].cpu().numpy(), orf[0])
+
+
+def test_detect_large_exemplar_count():
+    """16 exemplars per image (config E fan-out) through TMREngine.detect:
+    every image's union and keep list equal the oracle's NMS over the GPU's
+    own candidates."""
+    B, E, hf = 2, 16, 24
+    P = synth.reference_state_dict(7, cin=32, emb=64, obj_bias=-0.2)
+    feats = cuda(synth.sam_features(21, B, 32, hf, hf))
+    ex, _ = synth.exemplar_set(22, B, E, 2 * hf, 2 * hf, 1, 31)
+    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=64))
+    L, Bx, R = eng.detect(feats, ex, 0.3, 0.5)
+    r = eng.forward_units(feats, np.repeat(np.arange(B), E), ex.reshape(-1, 4))
+    o, bb = r["o"].cpu().numpy(), r["b"].cpu().numpy()
+    for img in range(B):
+        ls, bs, rs = [], [], []
+        for e in range(E):
+            u = img * E + e
+            prob = oracle.sigmoid_cr(o[u, 0])
+            l_, b_, r_ = oracle.get_pred_boxes_prob([prob], [bb[u]], [ex[img, e:e + 1]], 0.3)
+            ls.append(l_[0]); bs.append(b_[0]); rs.append(r_[0])
+        ol, ob, orf = oracle.nms_lists([np.concatenate(ls)], [np.concatenate(bs)],
+                                       [np.concatenate(rs)], 0.5)
+        assert bits_equal(L[img].cpu().numpy(), ol[0])
+        assert bits_equal(Bx[img].cpu().numpy(), ob[0])
