@@ -146,6 +146,45 @@ int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, co
                         int leaky, const float *headw, const float *acc_init, float *partials,
                         void *stream);
 
+/* ---- (a11) split-precision 16-bit-MFMA variant of the decoder conv ---------
+ * Direct implicit-GEMM kxk conv (ks 1/3/5/7, pad ks/2) on
+ * v_mfma_f32_32x32x16_{f16,bf16}; same semantics as tmr_conv_store /
+ * tmr_conv_heads (regression_head.py:7-8, matching_net.py:63-75) except that
+ * operands are pre-packed 16-bit records:
+ *   TMR_PREC_F16X3: x*s = xh + xl, w*s' = wh + wl (fp16, power-of-two scales
+ *                   from the tensors' max |.|), x.w = (wh xh + wl xh + wh xl)
+ *                   / (s s') with fp32 accumulation: the fp32 path's 1e-5
+ *                   normwise contract (config B);
+ *   TMR_PREC_BF16:  one bf16 term, fp32 accumulation (config C, 1e-2 contract);
+ *   TMR_PREC_F16:   one scaled fp16 term.
+ * tmr_absmax: *out = max(|x|) (or max(*out, |x|) when accumulate), the scale
+ * source for the packs and the conv (F16X3 / F16; NULL allowed for BF16).
+ * tmr_split_xpack: x [S][C][H][W] fp32 -> [S][ceil(C/16)][Hp][Wp][rec], zero
+ * padded to whole 16x32 tiles plus the ks halo (sizes in BYTES).
+ * tmr_split_wpack: w [N][C0+C1][ks][ks] -> [ks*ks][ceil(C0/16)+ceil(C1/16)]
+ * [ceil(N/128)*128][rec]; the conv's src0 (per image, C0 channels, packed by
+ * xpack with S = images) and src1 (per unit, C1) may both be present.
+ * Head partials use 128-channel tiles (tmr_heads_reduce tile_n = 128). */
+#define TMR_PREC_F16X3 0
+#define TMR_PREC_BF16 1
+#define TMR_PREC_F16 2
+int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stream);
+int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec);
+int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
+                    const float *xmax, void *out, void *stream);
+int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec);
+int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, const float *wmax,
+                    void *out, void *stream);
+int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
+                         int C1, int U, int H, int W, int ks, int prec, const void *wpack,
+                         const float *wmax, const float *xmax, const float *bias, int N,
+                         int leaky, const float *acc_init, float *out, void *stream);
+int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
+                         int C1, int U, int H, int W, int ks, int prec, const void *wpack,
+                         const float *wmax, const float *xmax, const float *bias, int N,
+                         int leaky, const float *headw, const float *acc_init,
+                         float *partials, void *stream);
+
 /* ---- (a14-a16) peak finder + box decode ------------------------------------
  * Get_pred_boxes per unit (utils/TM_utils.py:245-282): p = sigmoid(o) (or o
  * itself when input_is_prob), masked 3x3 local max with zero padding,

@@ -19,9 +19,10 @@ from tmr_import import load_package  # noqa: E402
 
 tmr = load_package()
 from tmr_amd._lib import call, load, ptr, stream  # noqa: E402
-from tmr_amd.engine import pack_conv, pack_wino  # noqa: E402
+from tmr_amd.engine import absmax, pack_conv, pack_split_w, pack_split_x, pack_wino  # noqa: E402
 
 FP32_PEAK = 157.3
+F16_PEAK = 2516.6  # dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 
 
 def timeit(fn, reps):
@@ -52,6 +53,9 @@ def main():
     acc0 = torch.randn(U, N, H, W, device=dev) * 0.1
     part = torch.empty(load().tmr_heads_partials_size(N, U, H, W), device=dev)
     uw, dw = pack_wino(w), pack_conv(w)
+    sp = {p: pack_split_w(w, 0, p) for p in ("fp32", "bf16")}
+    xmax = absmax(x)
+    xs = {p: pack_split_x(x, 3, p, xmax) for p in ("fp32", "bf16")}
     out = torch.empty(U, N, H, W, device=dev)
     ui = torch.arange(U, device=dev, dtype=torch.int32)
     res = {"units": U, "H": H, "K_channels": C, "N": N}
@@ -66,15 +70,33 @@ def main():
         "direct_heads": (lambda: call("tmr_conv_heads", None, 0, ptr(ui), ptr(x), C, U, H, W, ptr(dw),
                                       ptr(b), N, 3, 1, ptr(hw), ptr(acc0), ptr(part), stream()), fl_d),
     }
+    for p, terms in (("fp32", 3), ("bf16", 1)):
+        pc = {"fp32": 0, "bf16": 1}[p]
+        runs[f"split_{p}_heads"] = (
+            lambda p=p, pc=pc: call("tmr_split_conv_heads", None, 0, ptr(ui), ptr(xs[p]), C, U, H, W, 3,
+                                    pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1, ptr(hw),
+                                    ptr(acc0), ptr(part), stream()), fl_d, terms)
+        runs[f"split_{p}_store"] = (
+            lambda p=p, pc=pc: call("tmr_split_conv_store", ptr(xs[p]), C, None, None, 0, U, H, W, 3,
+                                    pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 0, None,
+                                    ptr(out), stream()), fl_d, terms)
+        runs[f"split_{p}_xpack"] = (lambda p=p: pack_split_x(x, 3, p, xmax), 0.0, 0)
     if os.environ.get("KB_ONLY"):
         runs = {k: v for k, v in runs.items() if k in os.environ["KB_ONLY"].split(",")}
-    for name, (fn, fl) in runs.items():
+    for name, spec in runs.items():
+        fn, fl = spec[0], spec[1]
         fn()
         torch.cuda.synchronize()
         ms = timeit(fn, a.reps)
-        res[name] = {"ms": round(ms, 3), "executed_tflops": round(fl / ms / 1e9, 2),
-                     "frac_fp32_peak": round(fl / ms / 1e9 / FP32_PEAK, 4),
-                     "direct_equiv_tflops": round(fl_d / ms / 1e9, 2)}
+        r = {"ms": round(ms, 3), "direct_equiv_tflops": round(fl_d / ms / 1e9, 2)}
+        if len(spec) == 3:  # split kernel: 16-bit MFMA work = terms x direct FLOPs
+            if spec[2]:
+                r["mfma16_tflops"] = round(spec[2] * fl / ms / 1e9, 2)
+                r["frac_f16_peak"] = round(spec[2] * fl / ms / 1e9 / F16_PEAK, 4)
+        else:
+            r["executed_tflops"] = round(fl / ms / 1e9, 2)
+            r["frac_fp32_peak"] = round(fl / ms / 1e9 / FP32_PEAK, 4)
+        res[name] = r
     print(json.dumps(res))
 
 

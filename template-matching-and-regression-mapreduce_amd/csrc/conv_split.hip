@@ -1,0 +1,625 @@
+// Split-precision direct implicit-GEMM kxk convolution on 16-bit MFMA
+// (v_mfma_f32_32x32x16_f16 / _bf16), gfx950.  Same semantics and ABI role as
+// conv_mfma.hip / conv_wino.hip (Decoder_model conv + LeakyReLU, optional
+// fused 1x1 heads; models/regression_head.py:7-8,31,50,
+// models/matching_net.py:63-75).
+//
+// Precision modes (TMR_PREC_*):
+//   F16X3  fp32-grade: x = s_x^-1 (xh + xl), w = s_w^-1 (wh + wl) with fp16
+//          hi/lo parts and power-of-two scales s (max |x s| < 2^14), and
+//          x.w ~= (wh xh + wl xh + wh xl) / (s_x s_w), fp32 accumulation.
+//          The dropped wl xl term and the split residuals are ~2^-22
+//          relative: the result keeps the fp32 path's 1e-5 contract at 1/16
+//          of the MFMA cost of f32-input MFMA x 3 terms.
+//   BF16   one bf16 term (unscaled), fp32 accumulation (config C).
+//   F16    one scaled fp16 term.
+//
+// GEMM view: D[n][pixel] = sum_{tap, c} Wt[tap][n][c] X[c][pixel + tap], A =
+// weights (rows n), B = activations (columns = 32 consecutive pixels of one
+// output row), so a 32x32 accumulator register is one 128-B row segment of
+// the NCHW output (coalesced stores / acc_init loads).
+//
+// Operands live in HBM in MFMA-ready 16-bit layouts written by the pack
+// kernels below: per 16-channel chunk a pixel (or output channel) is one
+// record of P 16-B pieces [hi ch0-7][hi ch8-15]([lo ch0-7][lo ch8-15]).
+// Activations are zero-padded to whole tiles plus the kxk halo, so the
+// kernel's loads are never masked.
+//
+// Block: 512 threads, 128 output channels x 512 pixels (16 rows x 32 cols).
+// Waves 2 (64 n) x 4 (4 rows); a wave owns 2x4 32x32 accumulators (128 regs).
+// K loop: chunk (16 channels) outer, tap inner.  Per step the 128xP weight
+// records stream into LDS by LDS-DMA (double buffered), and the next chunk's
+// (16+k-1)x(32+k-1) activation halo streams in spread over the first taps.
+// The global source addresses carry an XOR swizzle (piece ^ record bits) so
+// the ds_read_b128 fragment reads are bank-conflict free.
+#include <algorithm>
+
+#include "tmr_common.h"
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+constexpr int BM = 128;      // output channels per block
+constexpr int TH = 16;       // output rows per block
+constexpr int TW = 32;       // output cols per block
+constexpr int NTHREADS = 512;
+constexpr int NWAVES = 8;
+constexpr int CCH = 16;      // input channels per chunk
+constexpr int NHEAD = 5;
+
+template <int PREC> struct Prec;
+template <> struct Prec<TMR_PREC_F16X3> {
+    static constexpr int P = 4;
+    static constexpr bool SCALED = true;
+    typedef _Float16 E;
+    typedef h8 V;
+};
+template <> struct Prec<TMR_PREC_BF16> {
+    static constexpr int P = 2;
+    static constexpr bool SCALED = false;
+    typedef __bf16 E;
+    typedef b8 V;
+};
+template <> struct Prec<TMR_PREC_F16> {
+    static constexpr int P = 2;
+    static constexpr bool SCALED = true;
+    typedef _Float16 E;
+    typedef h8 V;
+};
+
+// power-of-two scale with max |x| * s < 2^14 (fp16 max 65504)
+__device__ __forceinline__ float split_scale(const float *m) {
+    if (!m) return 1.0f;
+    const float v = *m;
+    if (!(v > 0.0f && v <= 3.0e38f)) return 1.0f;
+    int e;
+    frexpf(v, &e);  // v < 2^e
+    return ldexpf(1.0f, 14 - e);
+}
+
+template <int P>
+__device__ __forceinline__ int swz(int rec) {
+    return P == 4 ? ((rec >> 2) & 3) : ((rec >> 3) & 1);
+}
+
+__device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mma(b8 a, b8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// one 16-channel record: 16 fp32 values -> P pieces of 8 x 16-bit
+template <int PREC>
+__device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
+                                             typename Prec<PREC>::V (&out)[Prec<PREC>::P]) {
+    typedef typename Prec<PREC>::E E;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float xs = v[g * 8 + j] * s;
+            const E hi = (E)xs;
+            out[g][j] = hi;
+            if (Prec<PREC>::P == 4) out[2 + g][j] = (E)(xs - (float)hi);
+        }
+}
+
+struct SArgs {
+    const char *x0;   // packed src0 [img][NC0][Hp][Wp][rec]
+    const char *x1;   // packed src1 [u][NC1][Hp][Wp][rec]
+    const int32_t *unit_image;
+    const char *wp;   // packed weights [tap][NC0+NC1][Npad][rec]
+    const float *wmax, *xmax;
+    const float *bias, *headw, *acc_init;
+    float *out, *partials;
+    int NC0, NC1, U, H, W, N, NT, MT, TXN, Hp, Wp, Npad, leaky;
+};
+
+template <int KS, int PREC, int EPI>
+__global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
+    typedef Prec<PREC> PR;
+    typedef typename PR::V V;
+    constexpr int P = PR::P;
+    constexpr int REC = P * 16;                  // bytes per record
+    constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
+    constexpr int NPH = HR * HC * P;             // halo pieces (16 B)
+    constexpr int NIH = (NPH + 63) / 64;         // halo DMA wave-instructions
+    constexpr int HB = NIH * 1024;               // bytes per halo buffer
+    constexpr int NIW = BM * P / 64;             // weight DMA wave-instructions
+    constexpr int WB = NIW * 1024;
+    constexpr int T = KS * KS;
+    constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;  // halo instructions per wave per chunk
+    constexpr int Q = (MPW + T - 1) / T;              // ... issued per tap
+    constexpr int TERMS = P == 4 ? 3 : 1;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    char *Hs = lds;           // [2][HB]
+    char *Ws = lds + 2 * HB;  // [2][WB]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int l32 = lane & 31, h = lane >> 5;
+    const int wn = wave & 1, wpix = wave >> 1;
+
+    // XCD-aware bijective remap (the 8 XCDs take blocks round robin): the NT
+    // channel tiles of a pixel tile run back to back on one XCD and share its
+    // halo through L2.
+    const int nblk = gridDim.x, orig = blockIdx.x;
+    const int q8 = nblk >> 3, r8 = nblk & 7, xcd = orig & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    const int nt = L % a.NT;
+    const int rest = L / a.NT;
+    const int mt = rest % a.MT, u = rest / a.MT;
+    const int ty0 = (mt / a.TXN) * TH, tx0 = (mt % a.TXN) * TW;
+    const int img = a.unit_image ? a.unit_image[u] : u;
+    const int NC = a.NC0 + a.NC1;
+
+    // chunk-invariant per-lane DMA source offsets
+    int hoff[MPW];
+#pragma unroll
+    for (int m = 0; m < MPW; ++m) {
+        const int i = wave + NWAVES * m;
+        int e = i * 64 + lane;
+        if (e >= NPH) e = 0;  // pad pieces land past the image; any legal source
+        const int p = e / P, q = e % P;
+        const int hy = p / HC, hx = p % HC;
+        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + ((q ^ swz<P>(p)) * 16);
+    }
+    int woff;
+    {
+        const int e = (wave % NIW) * 64 + lane;
+        const int n = e / P, q = e % P;
+        woff = n * REC + ((q ^ swz<P>(n)) * 16);
+    }
+    const size_t cstride = (size_t)a.Hp * a.Wp * REC;
+    auto chunk_src = [&](int c) -> const char * {
+        return c < a.NC0 ? a.x0 + ((size_t)img * a.NC0 + c) * cstride
+                         : a.x1 + ((size_t)u * a.NC1 + (c - a.NC0)) * cstride;
+    };
+    auto halo_dma = [&](int c, int buf, int m0, int m1) {
+        const char *src = chunk_src(c);
+        char *dst = Hs + buf * HB;
+#pragma unroll
+        for (int m = 0; m < MPW; ++m) {
+            const int i = wave + NWAVES * m;
+            if (m >= m0 && m < m1 && i < NIH)
+                __builtin_amdgcn_global_load_lds((const void *)(src + hoff[m]),
+                                                 (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+        }
+    };
+    const char *wsrc0 = a.wp + (size_t)nt * BM * REC + woff;
+    auto w_dma = [&](int s, int buf) {
+        if (wave < NIW) {
+            const int c = s / T, tap = s % T;
+            const char *src = wsrc0 + ((size_t)tap * NC + c) * (size_t)a.Npad * REC;
+            __builtin_amdgcn_global_load_lds((const void *)src,
+                                             (lds_ptr_t)(Ws + buf * WB + wave * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    // fragment offsets that do not depend on the step
+    int aoff[2][TERMS];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int rec = wn * 64 + i * 32 + l32;
+#pragma unroll
+        for (int v = 0; v < TERMS; ++v) {
+            // F16X3: v0 = [wh|wl] x [xh|xh] (ch 0-7), v1 = same ch 8-15,
+            //        v2 = [wh g0|wh g1] x [xl g0|xl g1]
+            const int lq = TERMS == 3 ? (v == 0 ? 2 * h : v == 1 ? 2 * h + 1 : h) : h;
+            aoff[i][v] = rec * REC + ((lq ^ swz<P>(rec)) * 16);
+        }
+    }
+
+    const int S = NC * T;
+    halo_dma(0, 0, 0, MPW);
+    w_dma(0, 0);
+    __syncthreads();
+    for (int s = 0; s < S; ++s) {
+        const int c = s / T, tap = s - c * T;
+        const int ky = tap / KS, kx = tap - ky * KS;
+        if (s + 1 < S) w_dma(s + 1, (s + 1) & 1);
+        if (c + 1 < NC) halo_dma(c + 1, (c + 1) & 1, tap * Q, tap * Q + Q);
+        const char *wl = Ws + (s & 1) * WB;
+        const char *hl = Hs + (c & 1) * HB;
+        V af[2][TERMS];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int v = 0; v < TERMS; ++v) af[i][v] = *reinterpret_cast<const V *>(wl + aoff[i][v]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = (wpix * 4 + j + ky) * HC + l32 + kx;
+            V bf[TERMS];
+#pragma unroll
+            for (int v = 0; v < TERMS; ++v) {
+                const int lq = TERMS == 3 ? (v == 0 ? 0 : v == 1 ? 1 : 2 + h) : h;
+                bf[v] = *reinterpret_cast<const V *>(hl + p * REC + ((lq ^ swz<P>(p)) * 16));
+            }
+#pragma unroll
+            for (int v = 0; v < TERMS; ++v)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+        }
+        __syncthreads();  // drains this step's DMAs (vmcnt(0)) and frees the buffers
+    }
+
+    // ---------------- epilogue ----------------
+    float inv = 1.0f;
+    if (PR::SCALED) inv = 1.0f / (split_scale(a.xmax) * split_scale(a.wmax));  // 2^-k: exact
+    const int HW = a.H * a.W;
+    const int x = tx0 + l32;
+    const float *ai = a.acc_init ? a.acc_init + (size_t)img * a.N * HW : nullptr;
+    // the block's bias and head weights through LDS (the main loop's last
+    // barrier freed it): global loads here would be hoisted into registers
+    float *sb = reinterpret_cast<float *>(lds) + NHEAD * 16 * 32;  // past the head scratch
+    float *shw = sb + BM;                                           // [BM][NHEAD]
+    if (tid < BM) {
+        const int n = nt * BM + tid;
+        sb[tid] = n < a.N ? a.bias[n] : 0.0f;
+    }
+    if (EPI == 1)
+        for (int e = tid; e < BM * NHEAD; e += NTHREADS) shw[e] = a.headw[(size_t)nt * BM * NHEAD + e];
+    __syncthreads();
+    float hs[4][NHEAD];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < NHEAD; ++k) hs[j][k] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int nl = wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int n = nt * BM + nl;
+            const bool nin = n < a.N;
+            const float bn = sb[nl];
+            float hw[NHEAD];
+            if (EPI == 1) {
+#pragma unroll
+                for (int k = 0; k < NHEAD; ++k) hw[k] = shw[nl * NHEAD + k];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int y = ty0 + wpix * 4 + j;
+                const bool pin = nin && y < a.H && x < a.W;
+                const size_t pix = (size_t)y * a.W + x;
+                float v = acc[i][j][r] * inv;
+                if (ai && pin) v += ai[(size_t)n * HW + pix];
+                v += bn;
+                if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
+                if (EPI == 0) {
+                    if (pin) a.out[((size_t)u * a.N + n) * HW + pix] = v;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NHEAD; ++k) hs[j][k] = fmaf(v, hw[k], hs[j][k]);
+                }
+            }
+            // bound the acc_init loads in flight (32 per group): without it
+            // hipcc hoists all 128 ahead of the head FMAs and spills
+            if (EPI == 1 && (r & 7) == 7) asm volatile("" ::: "memory");
+        }
+    if (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < NHEAD; ++k) hs[j][k] += __shfl_xor(hs[j][k], 32);
+        float *red = reinterpret_cast<float *>(lds);  // [4 wpix][4 j][NHEAD][32]
+        if (wn == 1 && h == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < NHEAD; ++k) red[((wpix * 4 + j) * NHEAD + k) * 32 + l32] = hs[j][k];
+        }
+        __syncthreads();
+        if (wn == 0 && h == 0 && x < a.W) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int y = ty0 + wpix * 4 + j;
+                if (y >= a.H) continue;
+#pragma unroll
+                for (int k = 0; k < NHEAD; ++k) {
+                    const float v = hs[j][k] + red[((wpix * 4 + j) * NHEAD + k) * 32 + l32];
+                    a.partials[(((size_t)nt * NHEAD + k) * a.U + u) * HW + (size_t)y * a.W + x] = v;
+                }
+            }
+        }
+    }
+}
+
+template <int KS, int PREC>
+constexpr size_t lds_bytes() {
+    constexpr int P = Prec<PREC>::P;
+    constexpr int NPH = (TH + KS - 1) * (TW + KS - 1) * P;
+    return 2 * (size_t)((NPH + 63) / 64) * 1024 + 2 * (size_t)(BM * P / 64) * 1024;
+}
+
+template <int KS, int PREC, int EPI>
+int launch_split(SArgs a, hipStream_t s) {
+    constexpr size_t lds = lds_bytes<KS, PREC>();
+    static_assert(lds <= 160 * 1024, "LDS");
+    static_assert((NHEAD * 16 * 32 + BM * (NHEAD + 1)) * 4 <= lds, "epilogue scratch");
+    auto kern = split_conv_kernel<KS, PREC, EPI>;
+    if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+        return TMR_E_HIP;
+    const int64_t blocks = (int64_t)a.NT * a.MT * a.U;
+    if (blocks <= 0) return TMR_OK;
+    TMR_REQUIRE(blocks < (1ll << 31));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHREADS), lds, s, a);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+template <int KS, int EPI>
+int dispatch_prec(int prec, const SArgs &a, hipStream_t s) {
+    switch (prec) {
+        case TMR_PREC_F16X3: return launch_split<KS, TMR_PREC_F16X3, EPI>(a, s);
+        case TMR_PREC_BF16: return launch_split<KS, TMR_PREC_BF16, EPI>(a, s);
+        case TMR_PREC_F16: return launch_split<KS, TMR_PREC_F16, EPI>(a, s);
+        default: return TMR_E_INVALID;
+    }
+}
+
+template <int EPI>
+int dispatch_ks(int ks, int prec, const SArgs &a, hipStream_t s) {
+    switch (ks) {
+        case 1: return dispatch_prec<1, EPI>(prec, a, s);
+        case 3: return dispatch_prec<3, EPI>(prec, a, s);
+        case 5: return dispatch_prec<5, EPI>(prec, a, s);
+        case 7: return dispatch_prec<7, EPI>(prec, a, s);
+        default: return TMR_E_INVALID;
+    }
+}
+
+inline int prec_pieces(int prec) { return prec == TMR_PREC_F16X3 ? 4 : 2; }
+inline bool prec_ok(int prec) {
+    return prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16;
+}
+inline bool ks_ok(int ks) { return ks == 1 || ks == 3 || ks == 5 || ks == 7; }
+inline int pad_h(int H, int ks) { return (int)tmr_cdiv(H, TH) * TH + ks - 1; }
+inline int pad_w(int W, int ks) { return (int)tmr_cdiv(W, TW) * TW + ks - 1; }
+
+// ---------------------------------------------------------------- packing
+__global__ void absmax_kernel(const float *__restrict__ x, int64_t n, unsigned *__restrict__ out) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // m >= 0: uint order
+}
+
+__global__ void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4, unsigned *__restrict__ out) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = x[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// x [S][C][H][W] fp32 -> [S][ceil(C/16)][Hp][Wp][P x 16 B], zero padded:
+// padded (yp, xp) holds x[yp - ks/2][xp - ks/2].  One thread per record.
+template <int PREC>
+__global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, int W, int NCc,
+                             int Hp, int Wp, int pad, const float *__restrict__ xmax,
+                             typename Prec<PREC>::V *__restrict__ out) {
+    constexpr int P = Prec<PREC>::P;
+    const int64_t total = (int64_t)S * NCc * Hp * Wp;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int xp = (int)(i % Wp);
+    int64_t r = i / Wp;
+    const int yp = (int)(r % Hp);
+    r /= Hp;
+    const int c = (int)(r % NCc);
+    const int s = (int)(r / NCc);
+    const int y = yp - pad, xx = xp - pad;
+    const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
+    const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
+    float v[CCH];
+#pragma unroll
+    for (int k = 0; k < CCH; ++k) {
+        const int ch = c * CCH + k;
+        v[k] = (in && ch < C) ? x[(((size_t)s * C + ch) * H + y) * W + xx] : 0.0f;
+    }
+    typename Prec<PREC>::V rec[P];
+    split_record<PREC>(v, sc, rec);
+#pragma unroll
+    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
+}
+
+// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][P x 16 B]; the src0
+// and src1 channel ranges are padded to whole chunks separately.
+template <int PREC>
+__global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1, int ks, int NC0,
+                             int NC, int Npad, const float *__restrict__ wmax,
+                             typename Prec<PREC>::V *__restrict__ out) {
+    constexpr int P = Prec<PREC>::P;
+    const int T = ks * ks;
+    const int64_t total = (int64_t)T * NC * Npad;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int n = (int)(i % Npad);
+    int64_t r = i / Npad;
+    const int c = (int)(r % NC);
+    const int tap = (int)(r / NC);
+    const int C = C0 + C1;
+    const float sc = Prec<PREC>::SCALED ? split_scale(wmax) : 1.0f;
+    float v[CCH];
+#pragma unroll
+    for (int k = 0; k < CCH; ++k) {
+        int ch;
+        bool ok;
+        if (c < NC0) {
+            ch = c * CCH + k;
+            ok = ch < C0;
+        } else {
+            const int c1 = (c - NC0) * CCH + k;
+            ch = C0 + c1;
+            ok = c1 < C1;
+        }
+        v[k] = (ok && n < N) ? w[((size_t)n * C + ch) * T + tap] : 0.0f;
+    }
+    typename Prec<PREC>::V rec[P];
+    split_record<PREC>(v, sc, rec);
+#pragma unroll
+    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
+}
+
+int split_common(const void *xp0, int C0, const int32_t *unit_image, const void *xp1, int C1, int U,
+                 int H, int W, int ks, int prec, const void *wpack, const float *wmax,
+                 const float *xmax, const float *bias, int N, int leaky, const float *acc_init,
+                 float *out, const float *headw, float *partials, int epi, void *stream) {
+    TMR_REQUIRE(prec_ok(prec) && ks_ok(ks));
+    TMR_REQUIRE(wpack && bias && U > 0 && H > 0 && W > 0 && N > 0 && C0 >= 0 && C1 >= 0);
+    TMR_REQUIRE(C0 + C1 > 0 && (C0 == 0 || xp0) && (C1 == 0 || xp1));
+    TMR_REQUIRE(prec == TMR_PREC_BF16 || (wmax && xmax));
+    SArgs a = {};
+    a.x0 = static_cast<const char *>(xp0);
+    a.x1 = static_cast<const char *>(xp1);
+    a.unit_image = unit_image;
+    a.wp = static_cast<const char *>(wpack);
+    a.wmax = prec == TMR_PREC_BF16 ? nullptr : wmax;
+    a.xmax = prec == TMR_PREC_BF16 ? nullptr : xmax;
+    a.bias = bias;
+    a.headw = headw;
+    a.acc_init = acc_init;
+    a.out = out;
+    a.partials = partials;
+    a.NC0 = (int)tmr_cdiv(C0, CCH);
+    a.NC1 = (int)tmr_cdiv(C1, CCH);
+    a.U = U;
+    a.H = H;
+    a.W = W;
+    a.N = N;
+    a.NT = (int)tmr_cdiv(N, BM);
+    a.Npad = a.NT * BM;
+    a.TXN = (int)tmr_cdiv(W, TW);
+    a.MT = a.TXN * (int)tmr_cdiv(H, TH);
+    a.Hp = pad_h(H, ks);
+    a.Wp = pad_w(W, ks);
+    a.leaky = leaky;
+    hipStream_t s = tmr_stream(stream);
+    return epi ? dispatch_ks<1>(ks, prec, a, s) : dispatch_ks<0>(ks, prec, a, s);
+}
+
+}  // namespace
+
+extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stream) {
+    TMR_REQUIRE(out && n >= 0 && (n == 0 || x));
+    hipStream_t s = tmr_stream(stream);
+    if (!accumulate && hipMemsetAsync(out, 0, sizeof(float), s) != hipSuccess) return TMR_E_HIP;
+    if (n == 0) return TMR_OK;
+    unsigned *o = reinterpret_cast<unsigned *>(out);
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0) {
+        const int64_t n4 = n / 4;
+        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n4, 256), 4096);
+        hipLaunchKernelGGL(absmax_vec_kernel, dim3(blocks), dim3(256), 0, s,
+                           reinterpret_cast<const float4 *>(x), n4, o);
+    } else {
+        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n, 256), 4096);
+        hipLaunchKernelGGL(absmax_kernel, dim3(blocks), dim3(256), 0, s, x, n, o);
+    }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec) {
+    if (S <= 0 || C <= 0 || H <= 0 || W <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
+    return (int64_t)S * tmr_cdiv(C, CCH) * pad_h(H, ks) * pad_w(W, ks) * prec_pieces(prec) * 16;
+}
+
+extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
+                               const float *xmax, void *out, void *stream) {
+    TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
+    TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
+    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int64_t total = (int64_t)S * NCc * Hp * Wp;
+    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
+    hipStream_t s = tmr_stream(stream);
+    switch (prec) {
+        case TMR_PREC_F16X3:
+            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_F16X3>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
+                               Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+        case TMR_PREC_BF16:
+            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_BF16>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
+                               Wp, ks / 2, nullptr, static_cast<b8 *>(out));
+            break;
+        default:
+            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_F16>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
+                               Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+    }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec) {
+    if (N <= 0 || C0 < 0 || C1 < 0 || C0 + C1 <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
+    return (int64_t)ks * ks * (tmr_cdiv(C0, CCH) + tmr_cdiv(C1, CCH)) * tmr_cdiv(N, BM) * BM *
+           prec_pieces(prec) * 16;
+}
+
+extern "C" int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec,
+                               const float *wmax, void *out, void *stream) {
+    TMR_REQUIRE(w && out && N > 0 && C0 >= 0 && C1 >= 0 && C0 + C1 > 0 && ks_ok(ks) && prec_ok(prec));
+    TMR_REQUIRE(prec == TMR_PREC_BF16 || wmax);
+    const int NC0 = (int)tmr_cdiv(C0, CCH), NC = NC0 + (int)tmr_cdiv(C1, CCH);
+    const int Npad = (int)tmr_cdiv(N, BM) * BM;
+    const int64_t total = (int64_t)ks * ks * NC * Npad;
+    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
+    hipStream_t s = tmr_stream(stream);
+    switch (prec) {
+        case TMR_PREC_F16X3:
+            hipLaunchKernelGGL(wpack_kernel<TMR_PREC_F16X3>, grid, blk, 0, s, w, N, C0, C1, ks, NC0,
+                               NC, Npad, wmax, static_cast<h8 *>(out));
+            break;
+        case TMR_PREC_BF16:
+            hipLaunchKernelGGL(wpack_kernel<TMR_PREC_BF16>, grid, blk, 0, s, w, N, C0, C1, ks, NC0,
+                               NC, Npad, nullptr, static_cast<b8 *>(out));
+            break;
+        default:
+            hipLaunchKernelGGL(wpack_kernel<TMR_PREC_F16>, grid, blk, 0, s, w, N, C0, C1, ks, NC0,
+                               NC, Npad, wmax, static_cast<h8 *>(out));
+            break;
+    }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image,
+                                    const void *xp1, int C1, int U, int H, int W, int ks, int prec,
+                                    const void *wpack, const float *wmax, const float *xmax,
+                                    const float *bias, int N, int leaky, const float *acc_init,
+                                    float *out, void *stream) {
+    TMR_REQUIRE(out);
+    return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
+                        leaky, acc_init, out, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image,
+                                    const void *xp1, int C1, int U, int H, int W, int ks, int prec,
+                                    const void *wpack, const float *wmax, const float *xmax,
+                                    const float *bias, int N, int leaky, const float *headw,
+                                    const float *acc_init, float *partials, void *stream) {
+    TMR_REQUIRE(headw && partials);
+    return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
+                        leaky, acc_init, nullptr, headw, partials, 1, stream);
+}

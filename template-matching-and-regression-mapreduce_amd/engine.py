@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import host
-from ._lib import TMRError, call, load, ptr, require_gpu, stream
+from ._lib import PREC_CODES, TMRError, call, load, ptr, require_gpu, stream
 
 NHEAD = 5
 
@@ -43,6 +43,9 @@ class PathConfig:
     decoder_num_layer: int = 1
     decoder_kernel_size: int = 3
     no_matcher: bool = False
+    # decoder-conv arithmetic: "fp32" (3-term fp16 split on 16-bit MFMA, the
+    # fp32 1e-5 contract), "bf16" (config C, 1e-2 contract) or "f16"
+    precision: str = "fp32"
 
     @classmethod
     def from_args(cls, args) -> "PathConfig":
@@ -50,7 +53,8 @@ class PathConfig:
                    box_reg=not args.ablation_no_box_regression, template_type=args.template_type,
                    feature_upsample=bool(args.feature_upsample),
                    decoder_num_layer=args.decoder_num_layer,
-                   decoder_kernel_size=args.decoder_kernel_size, no_matcher=bool(args.no_matcher))
+                   decoder_kernel_size=args.decoder_kernel_size, no_matcher=bool(args.no_matcher),
+                   precision=getattr(args, "precision", "fp32"))
 
 
 def _version_key(ts: Sequence[torch.Tensor]):
@@ -100,6 +104,75 @@ def pack_wino(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """max |x| as a 1-element device tensor (max(out, |x|) when out is given)."""
+    require_gpu(x, "absmax input")
+    x = x.contiguous()
+    acc = out is not None
+    if out is None:
+        out = torch.empty(1, device=x.device, dtype=torch.float32)
+    call("tmr_absmax", ptr(x), x.numel(), int(acc), ptr(out), stream())
+    return out
+
+
+def prec_code(precision: str) -> int:
+    if precision not in PREC_CODES:
+        raise TMRError(f"precision must be one of {sorted(PREC_CODES)}, got {precision!r}")
+    return PREC_CODES[precision]
+
+
+def pack_split_w(w: torch.Tensor, c0: int, precision: str):
+    """[N,C0+C1,ks,ks] fp32 -> (16-bit packed weights, max|w|) for the split
+    conv kernel (include/tmr.h tmr_split_wpack)."""
+    require_gpu(w, "conv weight")
+    w = w.detach().float().contiguous()
+    N, C, ks, ks2 = w.shape
+    if ks != ks2:
+        raise TMRError("square kernels only (regression_head.py:7)")
+    pc = prec_code(precision)
+    n = load().tmr_split_wpack_size(N, c0, C - c0, ks, pc)
+    if n <= 0:
+        raise TMRError(f"unsupported conv shape {tuple(w.shape)}")
+    wmax = absmax(w)
+    out = torch.empty(n, device=w.device, dtype=torch.uint8)
+    call("tmr_split_wpack", ptr(w), N, c0, C - c0, ks, pc, ptr(wmax), ptr(out), stream())
+    return out, wmax
+
+
+def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -> torch.Tensor:
+    """[S,C,H,W] fp32 -> zero-padded 16-bit records (tmr_split_xpack)."""
+    require_gpu(x, "conv input")
+    x = x.float().contiguous()
+    S, C, H, W = x.shape
+    pc = prec_code(precision)
+    n = load().tmr_split_xpack_size(S, C, H, W, ks, pc)
+    if n <= 0:
+        raise TMRError(f"unsupported conv input {tuple(x.shape)}")
+    out = torch.empty(n, device=x.device, dtype=torch.uint8)
+    call("tmr_split_xpack", ptr(x), S, C, H, W, ks, pc, ptr(xmax), ptr(out), stream())
+    return out
+
+
+def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
+                 precision: str = "fp32", packed=None):
+    """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the split 16-bit
+    MFMA kernel (precision "fp32" keeps the 1e-5 contract)."""
+    require_gpu(x, "conv input")
+    x = x.float().contiguous()
+    U, C, H, W = x.shape
+    N, Cw, ks, _ = w.shape
+    if Cw != C:
+        raise TMRError(f"conv expects {Cw} input channels, got {C}")
+    wp, wmax = packed if packed is not None else pack_split_w(w, C, precision)
+    xmax = absmax(x)
+    xp = pack_split_x(x, ks, precision, xmax)
+    out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
+    call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, prec_code(precision),
+         ptr(wp), ptr(wmax), ptr(xmax), ptr(b.detach().float().contiguous()), N, int(leaky), None,
+         ptr(out), stream())
+    return out
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool, packed=None):
     """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the MFMA kernel."""
     require_gpu(x, "conv input")
@@ -133,9 +206,11 @@ class TMREngine:
         # per image when several exemplars share it (fp32, changes only the
         # summation order; same 1e-5 contract)
         self.share_fp_half = True
-        # 3x3 decoders: "wino" = Winograd F(2x2,3x3) kernel (16 instead of 36
-        # multiplies per 2x2 tile), "direct" = implicit GEMM over the 9 taps
-        self.decoder_algo = "wino" if cfg.decoder_kernel_size == 3 else "direct"
+        # decoder conv kernel: "split" = direct implicit GEMM on 16-bit MFMA
+        # (conv_split.hip, cfg.precision), "wino" = Winograd F(2x2,3x3) on
+        # fp32 MFMA, "direct" = implicit GEMM on fp32 MFMA
+        self.decoder_algo = "split"
+        prec_code(cfg.precision)
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -185,15 +260,32 @@ class TMREngine:
             no = layers[-1][0].shape[0]
             hw[n0:n0 + no, 4] = ow.detach().float().reshape(no)
             hb[4] = ob.detach().float().reshape(())
-            pk = pack_wino if algo == "wino" else pack_conv
+            c0_full = cfg.emb_dim if cfg.fusion else 0
+            if algo == "split":
+                prec = cfg.precision
+                pk = lambda w_, c0: pack_split_w(w_, c0, prec)  # noqa: E731
+            else:
+                pk0 = pack_wino if algo == "wino" else pack_conv
+                pk = lambda w_, c0: pk0(w_)  # noqa: E731
             split = None
             if split_c0:
-                split = (pk(W[:, :split_c0].contiguous()), pk(W[:, split_c0:].contiguous()),
+                split = (pk(W[:, :split_c0].contiguous(), split_c0), pk(W[:, split_c0:].contiguous(), 0),
                          torch.zeros(N, device=W.device, dtype=torch.float32))
-            full = None if split_c0 else pk(W)
+            full = None if split_c0 else pk(W, c0_full)
             return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
 
-        return self._cache.get(f"fused_dec{split_c0}_{algo}", tensors, build)
+        return self._cache.get(f"fused_dec{split_c0}_{algo}_{cfg.precision}", tensors, build)
+
+    def _conv(self, name: str, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool):
+        """One nn.Conv2d (+ LeakyReLU) of the general-depth stack on the
+        engine's decoder kernel."""
+        if self.decoder_algo == "split":
+            prec = self.cfg.precision
+            wp = self._cache.get(f"{name}_split_{prec}", [w],
+                                 lambda: pack_split_w(w, w.shape[1], prec))
+            return conv2d_split(x, w, b, leaky, prec, wp)
+        wp = self._cache.get(name, [w], lambda: pack_conv(w))
+        return conv2d(x, w, b, leaky, wp)
 
     # ------------------------------------------------------------ forward
     def project(self, feats: torch.Tensor, want_f0: bool = False):
@@ -252,8 +344,10 @@ class TMREngine:
             # when that removes work (U >= 2B): conv_fp once per image, then
             # the per-unit kernel starts from it and runs only the f_TM half
             share = self.share_fp_half and cfg.fusion and U >= 2 * B
-            algo = self.decoder_algo if cfg.decoder_kernel_size == 3 else "direct"
-            wino = algo == "wino"
+            algo = self.decoder_algo
+            if algo == "wino" and cfg.decoder_kernel_size != 3:
+                algo = "direct"
+            wino, splitk = algo == "wino", algo == "split"
             ks = cfg.decoder_kernel_size
             wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0, algo)
             if Cw != C0 + C1:
@@ -262,10 +356,27 @@ class TMREngine:
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
             acc0 = None
             C0k = C0
+            pc = prec_code(cfg.precision)
+            if splitk:
+                # 16-bit operand records; one activation scale per conv launch
+                # (both sources of a virtual concat share it)
+                if share:
+                    xmax0 = absmax(fp)
+                    xp0 = pack_split_x(fp, ks, cfg.precision, xmax0)
+                    xmax1 = absmax(f_tm)
+                else:
+                    xmax1 = absmax(fp) if src0 is not None else None
+                    xmax1 = absmax(f_tm, xmax1)
+                    xp0 = pack_split_x(fp, ks, cfg.precision, xmax1) if src0 is not None else None
+                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
             if share:
                 wp_fp, wp_tm, zero_b = split
                 acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
-                if wino:
+                if splitk:
+                    call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
+                         ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0, None,
+                         ptr(acc0), stream())
+                elif wino:
                     call("tmr_wino_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
                          ptr(zero_b), N, 0, None, ptr(acc0), stream())
                 else:
@@ -278,7 +389,11 @@ class TMREngine:
                 ev[0].record()
             s0 = ptr(src0) if src0 is not None else None
             a0 = ptr(acc0) if acc0 is not None else None
-            if wino:
+            if splitk:
+                call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
+                     U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
+                     a0, ptr(part), stream())
+            elif wino:
                 call("tmr_wino_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
                      ptr(bias), N, 1, ptr(hw), a0, ptr(part), stream())
             else:
@@ -291,7 +406,7 @@ class TMREngine:
                 tiles = ((H + 1) // 2) * ((W + 1) // 2)
                 self.last_decoder_flops = 2.0 * 16 * tiles * N * (C0k + C1) * U
                 self.last_shared_flops = 2.0 * 16 * tiles * N * C0 * B if share else 0.0
-            else:
+            else:  # direct conv (the split kernel executes 3 16-bit MFMA terms per product)
                 self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * ks ** 2 * U
                 self.last_shared_flops = 2.0 * H * W * N * C0 * ks ** 2 * B if share else 0.0
             self.last_decoder_algo = algo
@@ -306,17 +421,14 @@ class TMREngine:
         for pre in (["decoder_b"] if cfg.box_reg else []) + ["decoder_o"]:
             x = x0
             for l, (w, bb) in enumerate(self._dec_layers(pre)):
-                wp = self._cache.get(f"{pre}.{l}", [w], lambda w=w: pack_conv(w))
-                x = conv2d(x, w, bb, True, wp)
+                x = self._conv(f"{pre}.{l}", x, w, bb, True)
             res[pre] = x
         ow, ob = self.P["objectness_head.head.0.weight"], self.P["objectness_head.head.0.bias"]
-        o = conv2d(res["decoder_o"], ow, ob, False,
-                   self._cache.get("obj", [ow], lambda: pack_conv(ow)))
+        o = self._conv("obj", res["decoder_o"], ow, ob, False)
         b = None
         if cfg.box_reg:
             lw, lb = self.P["ltrbs_head.head.0.weight"], self.P["ltrbs_head.head.0.bias"]
-            b = conv2d(res["decoder_b"], lw, lb, False,
-                       self._cache.get("ltrbs", [lw], lambda: pack_conv(lw)))
+            b = self._conv("ltrbs", res["decoder_b"], lw, lb, False)
         return o, b
 
     def forward_units(self, feats: torch.Tensor, unit_image: Sequence[int], unit_boxes,

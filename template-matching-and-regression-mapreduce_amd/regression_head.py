@@ -2,8 +2,11 @@
 (reference: models/regression_head.py:3-62).
 
 Same constructors, reference initialisation (N(0, 0.01) weights, zero bias,
-:17-24) and state_dict keys (``layer.<2i>.weight``, ``head.0.weight``); the
-forwards run on the fp32 MFMA implicit-GEMM kernel (tmr_conv_store).  Inside
+:17-24) and state_dict keys (``layer.<2i>.weight``, ``head.0.weight``).
+``Decoder_model`` runs on the split 16-bit-MFMA implicit-GEMM kernel
+(tmr_split_conv_store; ``precision`` "fp32" = 3-term fp16 split, the fp32
+1e-5 contract; "bf16" = config C), the 1x1 heads on the fp32 MFMA kernel
+(tmr_conv_store).  Inside
 ``matching_net`` the decoders and heads are not called one by one: the
 fused kernel (tmr_conv_heads) consumes their parameters directly.
 """
@@ -11,7 +14,7 @@ from __future__ import annotations
 
 from torch import nn
 
-from .engine import conv2d
+from .engine import conv2d, conv2d_split
 
 
 class Decoder_model(nn.Module):
@@ -24,6 +27,7 @@ class Decoder_model(nn.Module):
             layer.append(nn.LeakyReLU())
         self.layer = nn.Sequential(*layer)
         self.out_channels = in_channels
+        self.precision = "fp32"
         self.reset_parameters()
 
     def convs(self):
@@ -31,7 +35,7 @@ class Decoder_model(nn.Module):
 
     def forward(self, x):
         for conv in self.convs():
-            x = conv2d(x, conv.weight, conv.bias, leaky=True)
+            x = conv2d_split(x, conv.weight, conv.bias, True, self.precision)
         return x
 
     def reset_parameters(self):

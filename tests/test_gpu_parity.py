@@ -172,6 +172,82 @@ def test_wino_conv_vs_torch(C, N, H, W, leaky):
     assert normwise(out.cpu().numpy(), ref.numpy()) <= TOL
 
 
+SPLIT_TOL = {"fp32": TOL, "f16": 1e-3, "bf16": 1e-2}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "f16"])
+@pytest.mark.parametrize("C,N,H,W,ks,leaky", [(64, 64, 32, 40, 3, True), (40, 72, 17, 33, 3, True),
+                                              (13, 200, 9, 70, 3, False), (1024, 256, 16, 32, 3, True),
+                                              (16, 16, 24, 24, 5, True), (24, 8, 20, 20, 1, False),
+                                              (12, 12, 9, 9, 7, True), (512, 2048, 16, 16, 3, True)])
+def test_split_conv_vs_torch(C, N, H, W, ks, leaky, prec):
+    """Split 16-bit MFMA kernel (tmr_split_conv_store) vs ATen conv2d (fp32
+    CPU) with an acc_init input: "fp32" (3-term fp16 split) within the 1e-5
+    contract, one-term bf16 / f16 within their stated tolerances."""
+    from tmr_amd._lib import PREC_CODES, call, ptr, stream
+    from tmr_amd.engine import absmax, pack_split_w, pack_split_x
+    torch.manual_seed(C * 7 + N + ks)
+    x = torch.randn(2, C, H, W)
+    w = torch.randn(N, C, ks, ks) * (1.0 / (ks * C ** 0.5))
+    b = torch.randn(N)
+    init = torch.randn(2, N, H, W)
+    ref = torch.nn.functional.conv2d(x, w, b, padding=ks // 2) + init
+    if leaky:
+        ref = torch.nn.functional.leaky_relu(ref, 0.01)
+    xd, wd, bd, initd = cuda(x), cuda(w), cuda(b), cuda(init)
+    wp, wmax = pack_split_w(wd, C, prec)
+    xmax = absmax(xd)
+    xp = pack_split_x(xd, ks, prec, xmax)
+    out = torch.empty((2, N, H, W), device=DEV)
+    call("tmr_split_conv_store", ptr(xp), C, None, None, 0, 2, H, W, ks, PREC_CODES[prec], ptr(wp),
+         ptr(wmax), ptr(xmax), ptr(bd), N, int(leaky), ptr(initd), ptr(out), stream())
+    torch.cuda.synchronize()
+    assert normwise(out.cpu().numpy(), ref.numpy()) <= SPLIT_TOL[prec]
+
+
+@pytest.mark.parametrize("scale", [1e-6, 1.0, 3e5])
+def test_split_conv_scales_and_two_sources(scale):
+    """Activations far from unit scale (the power-of-two split scale), zero
+    rows, and the two-source virtual concat (src0 per image via unit_image,
+    src1 per unit) of tmr_split_conv_heads vs the unsplit fp32 reference."""
+    from tmr_amd._lib import call, ptr, stream
+    from tmr_amd.engine import absmax, pack_split_w, pack_split_x
+    torch.manual_seed(3)
+    B, U, C0, C1, N, H, W = 2, 3, 24, 40, 136, 18, 35
+    x0 = torch.randn(B, C0, H, W) * scale
+    x1 = torch.randn(U, C1, H, W) * scale
+    x1[1] = 0.0
+    ui = np.array([1, 0, 1], np.int32)
+    w = torch.randn(N, C0 + C1, 3, 3) * 0.01
+    bias = torch.randn(N) * scale * 0.01
+    hw = torch.zeros(((N + 127) // 128) * 128, 5)
+    hw[:N] = torch.randn(N, 5)
+    xcat = torch.cat([x0[torch.from_numpy(ui).long()], x1], 1)
+    act = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(xcat.double(), w.double(),
+                                                                    bias.double(), padding=1), 0.01)
+    ref = torch.einsum("unhw,nj->ujhw", act, hw[:N].double()).numpy()
+    d = {k: cuda(v) for k, v in dict(x0=x0, x1=x1, w=w, b=bias, hw=hw).items()}
+    uid = cuda(torch.from_numpy(ui))
+    wp, wmax = pack_split_w(d["w"], C0, "fp32")
+    xmax = absmax(d["x1"], absmax(d["x0"]))
+    xp0 = pack_split_x(d["x0"], 3, "fp32", xmax)
+    xp1 = pack_split_x(d["x1"], 3, "fp32", xmax)
+    part = torch.empty(tmr_amd._lib.load().tmr_heads_partials_size(N, U, H, W), device=DEV)
+    call("tmr_split_conv_heads", ptr(xp0), C0, ptr(uid), ptr(xp1), C1, U, H, W, 3, 0, ptr(wp),
+         ptr(wmax), ptr(xmax), ptr(d["b"]), N, 1, ptr(d["hw"]), None, ptr(part), stream())
+    o = torch.empty((U, 1, H, W), device=DEV)
+    bb = torch.empty((U, 4, H, W), device=DEV)
+    hb = torch.zeros(5, device=DEV)
+    call("tmr_heads_reduce", ptr(part), N, 128, U, H, W, ptr(hb), ptr(o), ptr(bb), stream())
+    torch.cuda.synchronize()
+    got = np.concatenate([bb.cpu().numpy(), o.cpu().numpy()], 1)
+    for u in range(U):
+        if u == 1:
+            continue  # zero f_TM: only the src0 half contributes
+        assert normwise(got[u], ref[u]) <= TOL, u
+    assert normwise(got[1], ref[1]) <= TOL
+
+
 def test_wino_matches_direct_decoders():
     B, E = 2, 2
     P = synth.reference_state_dict(4, cin=64, emb=96, obj_bias=-0.3)
@@ -179,7 +255,7 @@ def test_wino_matches_direct_decoders():
     ex, _ = synth.exemplar_set(19, B, E, 40, 46, 3, 9)
     ui = np.repeat(np.arange(B), E)
     res = {}
-    for algo in ("wino", "direct"):
+    for algo in ("split", "wino", "direct"):
         for share in (True, False):
             eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=96))
             eng.decoder_algo, eng.share_fp_half = algo, share
@@ -422,3 +498,25 @@ def test_detect_large_exemplar_count():
                                        [np.concatenate(rs)], 0.5)
         assert bits_equal(L[img].cpu().numpy(), ol[0])
         assert bits_equal(Bx[img].cpu().numpy(), ob[0])
+
+
+@pytest.mark.parametrize("prec", ["bf16", "f16"])
+def test_reduced_precision_forward_vs_oracle(prec):
+    """Config-C style reduced-precision decoders (one 16-bit MFMA term, fp32
+    accumulation) at the scripted shape (emb 512, 128^2 maps, E=3): o and b
+    within the stated normwise tolerance of the fp32 torch-CPU oracle."""
+    B, E, hf = 1, 3, 64
+    P = oracle.reference_weights(0)
+    P["objectness_head.head.0.bias"] = torch.tensor([-1.0])
+    feats = synth.sam_features(5, B, 256, hf, hf)
+    ex, _ = synth.exemplar_set(70, B, E, 2 * hf, 2 * hf, 3, 15)
+    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(precision=prec))
+    ui = np.repeat(np.arange(B), E)
+    r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
+    assert eng.last_decoder_algo == "split"
+    o, b = r["o"].cpu().numpy(), r["b"].cpu().numpy()
+    for u in range(B * E):
+        exm = [torch.from_numpy(ex.reshape(-1, 4)[u:u + 1])]
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]), exm, P)
+        assert normwise(o[u], ro[0][0].numpy()) <= SPLIT_TOL[prec]
+        assert normwise(b[u], rb[0][0].numpy()) <= SPLIT_TOL[prec]
