@@ -38,6 +38,10 @@ from tmr_amd import driver, synth  # noqa: E402
 
 METRIC = "images/sec (whole node) match+regress+NMS; % HBM/MFMA roofline at 1/2/4/8 GPU"
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), spec
+# dense fp16/bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (MI355X_MICROARCH.md, ~2.5 PF)
+F16_PEAK_TFLOPS = 2516.6
+# 16-bit MFMA terms per product of the split decoder kernel (conv_split.hip)
+SPLIT_TERMS = {"fp32": 3, "bf16": 1, "f16": 1}
 EMB, CIN, KS = 512, 256, 3
 
 # BASELINE.json configs; B is the metric's headline workload
@@ -52,6 +56,9 @@ CONFIGS = {
     "E": dict(desc="config E (large-pattern stress): 8x SAM feats 256x96x96 (->192x192), 16 exemplars, "
                    "templates 3x3-31x31, fp32, cls 0.1, IoU 0.5", batch=8, E=16, hf=96, kmin=3, kmax=31,
               cls=0.1, iou=0.5),
+    "C": dict(desc="config C (FSCD-147 eval shape): 64x SAM feats 256x64x64 (->128x128), 3 shots, "
+                   "templates 3x3-15x15, bf16 MFMA decoders (fp32 accumulate), cls 0.25, IoU 0.5",
+              batch=64, E=3, hf=64, kmin=3, kmax=15, cls=0.25, iou=0.5, precision="bf16"),
 }
 H = W = 128  # set from the config in main()
 
@@ -94,14 +101,17 @@ def cpu_baseline(P, feats, ex, seconds: float, cls: float, iou: float):
                       f"{dt:.1f} s, torch {torch.__version__} CPU ({threads} threads)"}
 
 
-def load_traffic():
+def load_traffic(algo: str, prec: str):
     """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, raw) of the decoder
     kernel from the committed rocprofv3 PMC summary of the current kernel
-    version (profiles/decoder_pmc.json), or None."""
+    version (profiles/decoder_pmc.json, keyed by kernel variant), or None."""
     p = os.path.join(REPO, "profiles", "decoder_pmc.json")
     if os.path.exists(p):
         with open(p) as fh:
-            return json.load(fh).get("hbm_bytes_per_launch")
+            d = json.load(fh)
+        rec = d.get(f"{algo}_{prec}") if isinstance(d.get(f"{algo}_{prec}"), dict) else None
+        if rec is not None:
+            return rec.get("hbm_bytes_per_launch")
     return None
 
 
@@ -113,6 +123,9 @@ def main():
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="images per GPU per step")
     ap.add_argument("--exemplars", type=int, default=None)
+    ap.add_argument("--precision", default=None, choices=sorted(SPLIT_TERMS),
+                    help="decoder arithmetic (default: the config's; fp32 = 3-term fp16 split)")
+    ap.add_argument("--decoder", default="split", choices=["split", "wino", "direct"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
@@ -127,7 +140,9 @@ def main():
     cfg = CONFIGS[a.config]
     H = W = 2 * cfg["hf"]
     P = synth.reference_state_dict(0, device=dev)
-    eng = tmr.TMREngine(P, tmr.PathConfig())
+    prec = a.precision or cfg.get("precision", "fp32")
+    eng = tmr.TMREngine(P, tmr.PathConfig(precision=prec))
+    eng.decoder_algo = a.decoder
     B = a.batch or cfg["batch"]
     E = a.exemplars or cfg["E"]
     feats = synth.sam_features(1000 + rank, B, CIN, H // 2, W // 2)
@@ -173,7 +188,20 @@ def main():
         direct_equiv = 2.0 * H * W * (4 * EMB) * (EMB * KS * KS) * B * E
         if eng.last_shared_flops == 0.0:  # unshared (E == 1): the launch covers both halves
             direct_equiv *= 2
-        if eng.last_decoder_algo == "wino":
+        algo = eng.last_decoder_algo
+        peak, terms = FP32_PEAK_TFLOPS, 1
+        if algo == "split":
+            terms = SPLIT_TERMS[prec]
+            peak = F16_PEAK_TFLOPS
+            kernel_name = ("tmr_split_conv_heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
+                           "+ LeakyReLU + 1x1 heads, v_mfma_f32_32x32x16_%s)"
+                           % ("bf16" if prec == "bf16" else "f16"))
+            flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
+                           "(%s; the fp half runs once per image in tmr_split_conv_store and is "
+                           "shared by its exemplars; K=1024*9 when E=1)"
+                           % (terms, "fp32-grade 3-term fp16 split: hi*hi + lo*hi + hi*lo"
+                              if terms == 3 else "one %s term" % prec))
+        elif algo == "wino":
             kernel_name = ("tmr_wino_conv_heads (Winograd F(2x2,3x3) decoder_b+decoder_o f_TM half "
                            "+ LeakyReLU + 1x1 heads, fp32 MFMA 32x32x2)")
             flops_basis = ("executed: 16 transform-domain GEMMs, 2*16*(H/2*W/2)*N(2048)*K per unit "
@@ -182,20 +210,23 @@ def main():
         else:
             kernel_name = "tmr_conv_heads (direct decoder_b+decoder_o f_TM half + heads)"
             flops_basis = "executed: 2*H*W*N(2048)*K(512*9) per unit (f_TM half)"
+        achieved *= terms
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if prec == "bf16" else ("fp16" if prec == "f16" else "fp32"),
             "data": "synthetic (portable-PRNG SAM-like features, reference-init weights)",
             "config": {"workload": cfg["desc"], "config": a.config,
                        "images_per_gpu": B, "exemplars": E, "feature": [CIN, H // 2, W // 2],
                        "matching_map": [EMB, H, W], "parallelism": f"dp{world}",
-                       "mean_kept_per_image": round(float(np.mean(kept)), 1)},
+                       "mean_kept_per_image": round(float(np.mean(kept)), 1),
+                       "decoder": algo, "decoder_precision": prec},
             "roofline": {"bound": "mfma", "kernel": kernel_name,
-                         "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                         "traffic": load_traffic(), "avg_launch_ms": round(1e3 * avg_s, 3),
-                         "flops_per_launch": flops, "flops_basis": flops_basis,
+                         "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "traffic": load_traffic(algo, prec), "avg_launch_ms": round(1e3 * avg_s, 3),
+                         "flops_per_launch": flops * terms, "flops_basis": flops_basis,
                          "direct_conv_equivalent_tflops": round(direct_equiv / avg_s / 1e12, 2),
                          "path_algorithmic_tflop_per_step": round(
                              decoder_flops_per_unit() * B * E / 1e12, 2)},

@@ -13,6 +13,9 @@
 //          of the MFMA cost of f32-input MFMA x 3 terms.
 //   BF16   one bf16 term (unscaled), fp32 accumulation (config C).
 //   F16    one scaled fp16 term.
+// Every record is four 16-B pieces (64 B): F16X3 holds 16 channels as
+// [hi ch0-7][hi ch8-15][lo ch0-7][lo ch8-15] (3 MFMAs per 32x32 tile per
+// chunk), BF16/F16 hold 32 channels [ch0-7]..[ch24-31] (2 MFMAs).
 //
 // GEMM view: D[n][pixel] = sum_{tap, c} Wt[tap][n][c] X[c][pixel + tap], A =
 // weights (rows n), B = activations (columns = 32 consecutive pixels of one
@@ -20,18 +23,20 @@
 // the NCHW output (coalesced stores / acc_init loads).
 //
 // Operands live in HBM in MFMA-ready 16-bit layouts written by the pack
-// kernels below: per 16-channel chunk a pixel (or output channel) is one
-// record of P 16-B pieces [hi ch0-7][hi ch8-15]([lo ch0-7][lo ch8-15]).
+// kernels below: per channel chunk a pixel (or output channel) is one
+// 64-B record.
 // Activations are zero-padded to whole tiles plus the kxk halo, so the
 // kernel's loads are never masked.
 //
 // Block: 512 threads, 128 output channels x 512 pixels (16 rows x 32 cols).
 // Waves 2 (64 n) x 4 (4 rows); a wave owns 2x4 32x32 accumulators (128 regs).
-// K loop: chunk (16 channels) outer, tap inner.  Per step the 128xP weight
-// records stream into LDS by LDS-DMA (double buffered), and the next chunk's
-// (16+k-1)x(32+k-1) activation halo streams in spread over the first taps.
-// The global source addresses carry an XOR swizzle (piece ^ record bits) so
-// the ds_read_b128 fragment reads are bank-conflict free.
+// K loop: chunk outer, tap inner.  The 128 weight records of step s+2 stream
+// into LDS by LDS-DMA (3 buffers) while step s computes, and the next chunk's
+// (16+k-1)x(32+k-1) activation halo (2 buffers) streams in spread over the
+// first taps; each step ends with a counted vmcnt (only the DMAs the step
+// needs next) and a raw s_barrier, so loads stay in flight across barriers.
+// In LDS a record is padded to 80 B, which makes the ds_read_b128 fragment
+// reads bank-conflict free with plain linear addresses (immediate offsets).
 #include <algorithm>
 
 #include "tmr_common.h"
@@ -48,28 +53,35 @@ constexpr int TH = 16;       // output rows per block
 constexpr int TW = 32;       // output cols per block
 constexpr int NTHREADS = 512;
 constexpr int NWAVES = 8;
-constexpr int CCH = 16;      // input channels per chunk
 constexpr int NHEAD = 5;
 
 template <int PREC> struct Prec;
 template <> struct Prec<TMR_PREC_F16X3> {
-    static constexpr int P = 4;
+    static constexpr int CCH = 16;   // channels per record
+    static constexpr int TERMS = 3;  // MFMAs per 32x32 tile per chunk
     static constexpr bool SCALED = true;
     typedef _Float16 E;
     typedef h8 V;
 };
 template <> struct Prec<TMR_PREC_BF16> {
-    static constexpr int P = 2;
+    static constexpr int CCH = 32;
+    static constexpr int TERMS = 2;
     static constexpr bool SCALED = false;
     typedef __bf16 E;
     typedef b8 V;
 };
 template <> struct Prec<TMR_PREC_F16> {
-    static constexpr int P = 2;
+    static constexpr int CCH = 32;
+    static constexpr int TERMS = 2;
     static constexpr bool SCALED = true;
     typedef _Float16 E;
     typedef h8 V;
 };
+constexpr int P = 4;       // 16-B pieces per record in HBM
+constexpr int REC = 64;    // bytes per record in HBM
+constexpr int LP = 5;      // 16-B pieces per record in LDS (one pad piece)
+constexpr int LREC = 80;   // bytes per record in LDS
+constexpr int MAXCCH = 32;
 
 // power-of-two scale with max |x| * s < 2^14 (fp16 max 65504)
 __device__ __forceinline__ float split_scale(const float *m) {
@@ -81,9 +93,19 @@ __device__ __forceinline__ float split_scale(const float *m) {
     return ldexpf(1.0f, 14 - e);
 }
 
-template <int P>
-__device__ __forceinline__ int swz(int rec) {
-    return P == 4 ? ((rec >> 2) & 3) : ((rec >> 3) & 1);
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
 }
 
 __device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
@@ -93,20 +115,27 @@ __device__ __forceinline__ f32x16 mma(b8 a, b8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// one 16-channel record: 16 fp32 values -> P pieces of 8 x 16-bit
+// one record: CCH fp32 values -> 4 pieces of 8 x 16-bit
 template <int PREC>
-__device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
-                                             typename Prec<PREC>::V (&out)[Prec<PREC>::P]) {
+__device__ __forceinline__ void split_record(const float (&v)[MAXCCH], float s,
+                                             typename Prec<PREC>::V (&out)[P]) {
     typedef typename Prec<PREC>::E E;
+    if (Prec<PREC>::TERMS == 3) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+        for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float xs = v[g * 8 + j] * s;
-            const E hi = (E)xs;
-            out[g][j] = hi;
-            if (Prec<PREC>::P == 4) out[2 + g][j] = (E)(xs - (float)hi);
-        }
+            for (int j = 0; j < 8; ++j) {
+                const float xs = v[g * 8 + j] * s;
+                const E hi = (E)xs;
+                out[g][j] = hi;
+                out[2 + g][j] = (E)(xs - (float)hi);
+            }
+    } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) out[g][j] = (E)(v[g * 8 + j] * s);
+    }
 }
 
 struct SArgs {
@@ -120,28 +149,38 @@ struct SArgs {
     int NC0, NC1, U, H, W, N, NT, MT, TXN, Hp, Wp, Npad, leaky;
 };
 
+template <int KS>
+struct Geo {
+    static constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
+    static constexpr int NPH = HR * HC * LP;        // halo LDS pieces (16 B) incl. pads
+    static constexpr int NIH = (NPH + 63) / 64;     // halo DMA wave-instructions
+    static constexpr int HB = NIH * 1024;           // bytes per halo buffer
+    static constexpr int NIW = (BM * LP + 63) / 64; // weight DMA wave-instructions (10)
+    static constexpr int WB = NIW * 1024;
+    static constexpr int NWB = (2 * HB + 3 * WB <= 160 * 1024) ? 3 : 2;  // weight buffers
+    static constexpr int T = KS * KS;
+    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;  // halo instructions per wave per chunk
+    static constexpr int Q = (MPW + T - 1) / T;              // ... issued per tap
+    static constexpr int WPW = (NIW + NWAVES - 1) / NWAVES;  // weight instructions per wave per step
+    static constexpr size_t LDS = 2 * (size_t)HB + NWB * (size_t)WB;
+};
+
 template <int KS, int PREC, int EPI>
 __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     typedef Prec<PREC> PR;
     typedef typename PR::V V;
-    constexpr int P = PR::P;
-    constexpr int REC = P * 16;                  // bytes per record
-    constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
-    constexpr int NPH = HR * HC * P;             // halo pieces (16 B)
-    constexpr int NIH = (NPH + 63) / 64;         // halo DMA wave-instructions
-    constexpr int HB = NIH * 1024;               // bytes per halo buffer
-    constexpr int NIW = BM * P / 64;             // weight DMA wave-instructions
-    constexpr int WB = NIW * 1024;
-    constexpr int T = KS * KS;
-    constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;  // halo instructions per wave per chunk
-    constexpr int Q = (MPW + T - 1) / T;              // ... issued per tap
-    constexpr int TERMS = P == 4 ? 3 : 1;
+    typedef Geo<KS> G;
+    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH, NIW = G::NIW;
+    constexpr int HB = G::HB, WB = G::WB, NWB = G::NWB, WPW = G::WPW;
+    constexpr int D = NWB - 1;  // weight DMA lookahead (steps)
+    constexpr int TERMS = PR::TERMS;
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    char *Hs = lds;           // [2][HB]
-    char *Ws = lds + 2 * HB;  // [2][WB]
+    char *Hs = lds;           // [2][HB]   halo records [HR][HC][80 B]
+    char *Ws = lds + 2 * HB;  // [NWB][WB] weight records [BM][80 B]
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     const int l32 = lane & 31, h = lane >> 5;
     const int wn = wave & 1, wpix = wave >> 1;
 
@@ -158,110 +197,163 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int img = a.unit_image ? a.unit_image[u] : u;
     const int NC = a.NC0 + a.NC1;
 
-    // chunk-invariant per-lane DMA source offsets
+    // Per-lane DMA sources (chunk invariant).  LDS piece e of an image is
+    // record e / 5, slot e % 5; slot 4 is the pad (it re-reads piece 0 of
+    // the same 64-B line, no extra traffic) and pieces past the image land in
+    // the buffer's tail.
     int hoff[MPW];
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
         const int i = wave + NWAVES * m;
         int e = i * 64 + lane;
-        if (e >= NPH) e = 0;  // pad pieces land past the image; any legal source
-        const int p = e / P, q = e % P;
+        if (e >= G::NPH) e = 0;
+        const int p = e / LP, q = e % LP;
         const int hy = p / HC, hx = p % HC;
-        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + ((q ^ swz<P>(p)) * 16);
+        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + (q < P ? q : 0) * 16;
     }
-    int woff;
-    {
-        const int e = (wave % NIW) * 64 + lane;
-        const int n = e / P, q = e % P;
-        woff = n * REC + ((q ^ swz<P>(n)) * 16);
+    int woff[WPW];
+#pragma unroll
+    for (int m = 0; m < WPW; ++m) {
+        int e = (wave + NWAVES * m) * 64 + lane;
+        if (e >= BM * LP) e = 0;
+        const int n = e / LP, q = e % LP;
+        woff[m] = n * REC + (q < P ? q : 0) * 16;
     }
     const size_t cstride = (size_t)a.Hp * a.Wp * REC;
     auto chunk_src = [&](int c) -> const char * {
         return c < a.NC0 ? a.x0 + ((size_t)img * a.NC0 + c) * cstride
                          : a.x1 + ((size_t)u * a.NC1 + (c - a.NC0)) * cstride;
     };
-    auto halo_dma = [&](int c, int buf, int m0, int m1) {
+    // issue this wave's halo instructions m0 <= m < m1 of chunk c; returns the count
+    auto halo_dma = [&](int c, int m0, int m1) -> int {
         const char *src = chunk_src(c);
-        char *dst = Hs + buf * HB;
+        char *dst = Hs + (c & 1) * HB;
+        int n = 0;
 #pragma unroll
         for (int m = 0; m < MPW; ++m) {
             const int i = wave + NWAVES * m;
-            if (m >= m0 && m < m1 && i < NIH)
+            if (m >= m0 && m < m1 && i < NIH) {
                 __builtin_amdgcn_global_load_lds((const void *)(src + hoff[m]),
                                                  (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+                ++n;
+            }
         }
+        return n;
     };
-    const char *wsrc0 = a.wp + (size_t)nt * BM * REC + woff;
-    auto w_dma = [&](int s, int buf) {
-        if (wave < NIW) {
-            const int c = s / T, tap = s % T;
-            const char *src = wsrc0 + ((size_t)tap * NC + c) * (size_t)a.Npad * REC;
-            __builtin_amdgcn_global_load_lds((const void *)src,
-                                             (lds_ptr_t)(Ws + buf * WB + wave * 1024), 16, 0, 0);
-        }
-    };
-
-    f32x16 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-    // fragment offsets that do not depend on the step
-    int aoff[2][TERMS];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int rec = wn * 64 + i * 32 + l32;
-#pragma unroll
-        for (int v = 0; v < TERMS; ++v) {
-            // F16X3: v0 = [wh|wl] x [xh|xh] (ch 0-7), v1 = same ch 8-15,
-            //        v2 = [wh g0|wh g1] x [xl g0|xl g1]
-            const int lq = TERMS == 3 ? (v == 0 ? 2 * h : v == 1 ? 2 * h + 1 : h) : h;
-            aoff[i][v] = rec * REC + ((lq ^ swz<P>(rec)) * 16);
-        }
-    }
-
-    const int S = NC * T;
-    halo_dma(0, 0, 0, MPW);
-    w_dma(0, 0);
-    __syncthreads();
-    for (int s = 0; s < S; ++s) {
+    const char *wsrc0 = a.wp + (size_t)nt * BM * REC;
+    // weight buffer of step s = c*T + tap (compile-time when NWB divides T)
+    auto wbuf = [&](int s, int tap) -> int { return T % NWB == 0 ? tap % NWB : s % NWB; };
+    auto w_dma = [&](int s) -> int {
         const int c = s / T, tap = s - c * T;
-        const int ky = tap / KS, kx = tap - ky * KS;
-        if (s + 1 < S) w_dma(s + 1, (s + 1) & 1);
-        if (c + 1 < NC) halo_dma(c + 1, (c + 1) & 1, tap * Q, tap * Q + Q);
-        const char *wl = Ws + (s & 1) * WB;
-        const char *hl = Hs + (c & 1) * HB;
-        V af[2][TERMS];
+        const char *src = wsrc0 + ((size_t)tap * NC + c) * (size_t)a.Npad * REC;
+        char *dst = Ws + wbuf(s, tap) * WB;
+        int n = 0;
+#pragma unroll
+        for (int m = 0; m < WPW; ++m) {
+            const int i = wave + NWAVES * m;
+            if (i < NIW) {
+                __builtin_amdgcn_global_load_lds((const void *)(src + woff[m]),
+                                                 (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+                ++n;
+            }
+        }
+        return n;
+    };
+
+    // accumulators start at acc_init (scaled into the accumulator's units by
+    // the exact power of two s_x s_w); masked elements read a clamped legal
+    // address and are zeroed by a select, never by a branch around the load
+    const float sxw = PR::SCALED ? split_scale(a.xmax) * split_scale(a.wmax) : 1.0f;
+    const int HW = a.H * a.W;
+    const int x = tx0 + l32;
+    f32x16 acc[2][4];
+    if (a.acc_init) {
+        const float *ai = a.acc_init + (size_t)img * a.N * HW;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int v = 0; v < TERMS; ++v) af[i][v] = *reinterpret_cast<const V *>(wl + aoff[i][v]);
+            for (int j = 0; j < 4; ++j) {
+                const int y = ty0 + wpix * 4 + j;
+                const bool pin = y < a.H && x < a.W;
+                const int pix = min(y, a.H - 1) * a.W + min(x, a.W - 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int p = (wpix * 4 + j + ky) * HC + l32 + kx;
-            V bf[TERMS];
-#pragma unroll
-            for (int v = 0; v < TERMS; ++v) {
-                const int lq = TERMS == 3 ? (v == 0 ? 0 : v == 1 ? 1 : 2 + h) : h;
-                bf[v] = *reinterpret_cast<const V *>(hl + p * REC + ((lq ^ swz<P>(p)) * 16));
+                for (int r = 0; r < 16; ++r) {
+                    const int n = nt * BM + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float v = ai[(size_t)min(n, a.N - 1) * HW + pix];
+                    acc[i][j][r] = (pin && n < a.N) ? v * sxw : 0.0f;
+                }
             }
+    } else {
 #pragma unroll
-            for (int v = 0; v < TERMS; ++v)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    }
+
+    // fragment pieces: lane half h supplies k = 8h..8h+7 of each MFMA
+    //   F16X3: v0 = [wh|wl] x [xh|xh] (ch 0-7), v1 = same ch 8-15,
+    //          v2 = [wh g0|wh g1] x [xl g0|xl g1]
+    //   one term: v0 = ch 0-15, v1 = ch 16-31
+    // 80-B records: any 16 consecutive records hit 16 distinct 4-bank groups,
+    // so every ds_read_b128 below is conflict free with linear addresses and
+    // all per-step offsets fold into the instruction's immediate.
+    int aoff[TERMS], boff[TERMS];
+#pragma unroll
+    for (int v = 0; v < TERMS; ++v) {
+        const int aq = TERMS == 3 ? (v == 0 ? 2 * h : v == 1 ? 2 * h + 1 : h) : 2 * v + h;
+        const int bqv = TERMS == 3 ? (v == 0 ? 0 : v == 1 ? 1 : 2 + h) : 2 * v + h;
+        aoff[v] = (wn * 64 + l32) * LREC + aq * 16;
+        boff[v] = (wpix * 4 * HC + l32) * LREC + bqv * 16;
+    }
+
+    const int S = NC * T;
+    halo_dma(0, 0, MPW);
+    for (int s0 = 0; s0 < D && s0 < S; ++s0) w_dma(s0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int c = 0; c < NC; ++c) {
+        const char *hl = Hs + (c & 1) * HB;
+#pragma unroll
+        for (int tap = 0; tap < T; ++tap) {
+            const int s = c * T + tap;
+            const int ky = tap / KS, kx = tap % KS;
+            // DMAs for later steps: halo of chunk c+1 (buffer last read in
+            // chunk c-1), then the weights of step s+D (last read in s-1)
+            const int nh = (c + 1 < NC && tap * Q < MPW) ? halo_dma(c + 1, tap * Q, tap * Q + Q) : 0;
+            const int nw = s + D < S ? w_dma(s + D) : 0;
+            const char *wl = Ws + wbuf(s, tap) * WB;
+            V af[2][TERMS];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int v = 0; v < TERMS; ++v)
+                    af[i][v] = *reinterpret_cast<const V *>(wl + aoff[v] + i * 32 * LREC);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                V bf[TERMS];
+#pragma unroll
+                for (int v = 0; v < TERMS; ++v)
+                    bf[v] = *reinterpret_cast<const V *>(hl + boff[v] + ((j + ky) * HC + kx) * LREC);
+#pragma unroll
+                for (int v = 0; v < TERMS; ++v)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+            }
+            // the next step needs W(s+1) and, after a chunk's last tap, the
+            // whole halo of chunk c+1: leave only younger DMAs in flight
+            // (in-order completion; this step issued halo before weights)
+            if (D == 1)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else
+                wait_vmcnt(tap == T - 1 ? nw : nw + nh);
+            __builtin_amdgcn_s_barrier();
         }
-        __syncthreads();  // drains this step's DMAs (vmcnt(0)) and frees the buffers
     }
 
     // ---------------- epilogue ----------------
-    float inv = 1.0f;
-    if (PR::SCALED) inv = 1.0f / (split_scale(a.xmax) * split_scale(a.wmax));  // 2^-k: exact
-    const int HW = a.H * a.W;
-    const int x = tx0 + l32;
-    const float *ai = a.acc_init ? a.acc_init + (size_t)img * a.N * HW : nullptr;
+    const float inv = 1.0f / sxw;  // 2^-k: exact
     // the block's bias and head weights through LDS (the main loop's last
     // barrier freed it): global loads here would be hoisted into registers
     float *sb = reinterpret_cast<float *>(lds) + NHEAD * 16 * 32;  // past the head scratch
@@ -297,7 +389,6 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 const bool pin = nin && y < a.H && x < a.W;
                 const size_t pix = (size_t)y * a.W + x;
                 float v = acc[i][j][r] * inv;
-                if (ai && pin) v += ai[(size_t)n * HW + pix];
                 v += bn;
                 if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
                 if (EPI == 0) {
@@ -307,9 +398,6 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                     for (int k = 0; k < NHEAD; ++k) hs[j][k] = fmaf(v, hw[k], hs[j][k]);
                 }
             }
-            // bound the acc_init loads in flight (32 per group): without it
-            // hipcc hoists all 128 ahead of the head FMAs and spills
-            if (EPI == 1 && (r & 7) == 7) asm volatile("" ::: "memory");
         }
     if (EPI == 1) {
 #pragma unroll
@@ -339,16 +427,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     }
 }
 
-template <int KS, int PREC>
-constexpr size_t lds_bytes() {
-    constexpr int P = Prec<PREC>::P;
-    constexpr int NPH = (TH + KS - 1) * (TW + KS - 1) * P;
-    return 2 * (size_t)((NPH + 63) / 64) * 1024 + 2 * (size_t)(BM * P / 64) * 1024;
-}
-
 template <int KS, int PREC, int EPI>
 int launch_split(SArgs a, hipStream_t s) {
-    constexpr size_t lds = lds_bytes<KS, PREC>();
+    constexpr size_t lds = Geo<KS>::LDS;
     static_assert(lds <= 160 * 1024, "LDS");
     static_assert((NHEAD * 16 * 32 + BM * (NHEAD + 1)) * 4 <= lds, "epilogue scratch");
     auto kern = split_conv_kernel<KS, PREC, EPI>;
@@ -384,7 +465,7 @@ int dispatch_ks(int ks, int prec, const SArgs &a, hipStream_t s) {
     }
 }
 
-inline int prec_pieces(int prec) { return prec == TMR_PREC_F16X3 ? 4 : 2; }
+inline int prec_cch(int prec) { return prec == TMR_PREC_F16X3 ? Prec<TMR_PREC_F16X3>::CCH : Prec<TMR_PREC_BF16>::CCH; }
 inline bool prec_ok(int prec) {
     return prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16;
 }
@@ -413,13 +494,13 @@ __global__ void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4, unsi
     if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// x [S][C][H][W] fp32 -> [S][ceil(C/16)][Hp][Wp][P x 16 B], zero padded:
+// x [S][C][H][W] fp32 -> [S][ceil(C/CCH)][Hp][Wp][64 B], zero padded:
 // padded (yp, xp) holds x[yp - ks/2][xp - ks/2].  One thread per record.
 template <int PREC>
 __global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, int W, int NCc,
                              int Hp, int Wp, int pad, const float *__restrict__ xmax,
                              typename Prec<PREC>::V *__restrict__ out) {
-    constexpr int P = Prec<PREC>::P;
+    constexpr int CCH = Prec<PREC>::CCH;
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
@@ -432,11 +513,11 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, i
     const int y = yp - pad, xx = xp - pad;
     const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
     const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
-    float v[CCH];
+    float v[MAXCCH];
 #pragma unroll
-    for (int k = 0; k < CCH; ++k) {
+    for (int k = 0; k < MAXCCH; ++k) {
         const int ch = c * CCH + k;
-        v[k] = (in && ch < C) ? x[(((size_t)s * C + ch) * H + y) * W + xx] : 0.0f;
+        v[k] = (k < CCH && in && ch < C) ? x[(((size_t)s * C + ch) * H + y) * W + xx] : 0.0f;
     }
     typename Prec<PREC>::V rec[P];
     split_record<PREC>(v, sc, rec);
@@ -444,13 +525,13 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, i
     for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
 }
 
-// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][P x 16 B]; the src0
+// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][64 B]; the src0
 // and src1 channel ranges are padded to whole chunks separately.
 template <int PREC>
 __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1, int ks, int NC0,
                              int NC, int Npad, const float *__restrict__ wmax,
                              typename Prec<PREC>::V *__restrict__ out) {
-    constexpr int P = Prec<PREC>::P;
+    constexpr int CCH = Prec<PREC>::CCH;
     const int T = ks * ks;
     const int64_t total = (int64_t)T * NC * Npad;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -461,12 +542,15 @@ __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1,
     const int tap = (int)(r / NC);
     const int C = C0 + C1;
     const float sc = Prec<PREC>::SCALED ? split_scale(wmax) : 1.0f;
-    float v[CCH];
+    float v[MAXCCH];
 #pragma unroll
-    for (int k = 0; k < CCH; ++k) {
+    for (int k = 0; k < MAXCCH; ++k) {
         int ch;
         bool ok;
-        if (c < NC0) {
+        if (k >= CCH) {
+            ch = 0;
+            ok = false;
+        } else if (c < NC0) {
             ch = c * CCH + k;
             ok = ch < C0;
         } else {
@@ -502,8 +586,8 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     a.acc_init = acc_init;
     a.out = out;
     a.partials = partials;
-    a.NC0 = (int)tmr_cdiv(C0, CCH);
-    a.NC1 = (int)tmr_cdiv(C1, CCH);
+    a.NC0 = (int)tmr_cdiv(C0, prec_cch(prec));
+    a.NC1 = (int)tmr_cdiv(C1, prec_cch(prec));
     a.U = U;
     a.H = H;
     a.W = W;
@@ -542,14 +626,14 @@ extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out,
 
 extern "C" int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec) {
     if (S <= 0 || C <= 0 || H <= 0 || W <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
-    return (int64_t)S * tmr_cdiv(C, CCH) * pad_h(H, ks) * pad_w(W, ks) * prec_pieces(prec) * 16;
+    return (int64_t)S * tmr_cdiv(C, prec_cch(prec)) * pad_h(H, ks) * pad_w(W, ks) * REC;
 }
 
 extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
                                const float *xmax, void *out, void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
-    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int NCc = (int)tmr_cdiv(C, prec_cch(prec)), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
     const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
     hipStream_t s = tmr_stream(stream);
@@ -573,15 +657,16 @@ extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int k
 
 extern "C" int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec) {
     if (N <= 0 || C0 < 0 || C1 < 0 || C0 + C1 <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
-    return (int64_t)ks * ks * (tmr_cdiv(C0, CCH) + tmr_cdiv(C1, CCH)) * tmr_cdiv(N, BM) * BM *
-           prec_pieces(prec) * 16;
+    const int cc = prec_cch(prec);
+    return (int64_t)ks * ks * (tmr_cdiv(C0, cc) + tmr_cdiv(C1, cc)) * tmr_cdiv(N, BM) * BM * REC;
 }
 
 extern "C" int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec,
                                const float *wmax, void *out, void *stream) {
     TMR_REQUIRE(w && out && N > 0 && C0 >= 0 && C1 >= 0 && C0 + C1 > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || wmax);
-    const int NC0 = (int)tmr_cdiv(C0, CCH), NC = NC0 + (int)tmr_cdiv(C1, CCH);
+    const int cc = prec_cch(prec);
+    const int NC0 = (int)tmr_cdiv(C0, cc), NC = NC0 + (int)tmr_cdiv(C1, cc);
     const int Npad = (int)tmr_cdiv(N, BM) * BM;
     const int64_t total = (int64_t)ks * ks * NC * Npad;
     const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
