@@ -1,3 +1,5 @@
+# One GPU round: full -m gpu suite, bench B and C, rocprofv3 kernel trace, PMC traffic passes.
+# Run from the repo root: gpurun -- bash profiles/gpu_round.sh
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

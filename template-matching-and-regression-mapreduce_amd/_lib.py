@@ -15,6 +15,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtmr.so")
+if os.environ.get("TMR_LIB_VARIANT"):  # profiling only: an experiment build next to libtmr.so
+    LIB_PATH = os.path.join(_HERE, "libtmr_%s.so" % os.environ["TMR_LIB_VARIANT"])
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "tmr.h")
 
 _lock = threading.Lock()

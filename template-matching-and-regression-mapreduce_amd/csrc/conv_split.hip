@@ -30,13 +30,15 @@
 //
 // Block: 512 threads, 128 output channels x 512 pixels (16 rows x 32 cols).
 // Waves 2 (64 n) x 4 (4 rows); a wave owns 2x4 32x32 accumulators (128 regs).
-// K loop: chunk outer, tap inner.  The 128 weight records of step s+2 stream
-// into LDS by LDS-DMA (3 buffers) while step s computes, and the next chunk's
-// (16+k-1)x(32+k-1) activation halo (2 buffers) streams in spread over the
-// first taps; each step ends with a counted vmcnt (only the DMAs the step
-// needs next) and a raw s_barrier, so loads stay in flight across barriers.
-// In LDS a record is padded to 80 B, which makes the ds_read_b128 fragment
-// reads bank-conflict free with plain linear addresses (immediate offsets).
+// K loop: chunk outer, taps inner, up to 3 taps per barrier step.  The 128
+// weight records of step g+D stream into LDS by LDS-DMA (D+1 buffers) while
+// step g computes, and the next chunk's (16+k-1)x(32+k-1) activation halo
+// (2 buffers) streams in spread over the first steps; each step ends with a
+// counted vmcnt (only the DMAs the next step needs) and a raw s_barrier, so
+// loads stay in flight across barriers.
+// In LDS the records are stored as piece planes (structure of arrays), which
+// makes the ds_read_b128 fragment reads bank-conflict free with plain linear
+// addresses (immediate offsets).
 #include <algorithm>
 
 #include "tmr_common.h"
@@ -79,8 +81,6 @@ template <> struct Prec<TMR_PREC_F16> {
 };
 constexpr int P = 4;       // 16-B pieces per record in HBM
 constexpr int REC = 64;    // bytes per record in HBM
-constexpr int LP = 5;      // 16-B pieces per record in LDS (one pad piece)
-constexpr int LREC = 80;   // bytes per record in LDS
 constexpr int MAXCCH = 32;
 
 // power-of-two scale with max |x| * s < 2^14 (fp16 max 65504)
@@ -152,17 +152,31 @@ struct SArgs {
 template <int KS>
 struct Geo {
     static constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
-    static constexpr int NPH = HR * HC * LP;        // halo LDS pieces (16 B) incl. pads
-    static constexpr int NIH = (NPH + 63) / 64;     // halo DMA wave-instructions
-    static constexpr int HB = NIH * 1024;           // bytes per halo buffer
-    static constexpr int NIW = (BM * LP + 63) / 64; // weight DMA wave-instructions (10)
-    static constexpr int WB = NIW * 1024;
-    static constexpr int NWB = (2 * HB + 3 * WB <= 160 * 1024) ? 3 : 2;  // weight buffers
     static constexpr int T = KS * KS;
-    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;  // halo instructions per wave per chunk
-    static constexpr int Q = (MPW + T - 1) / T;              // ... issued per tap
-    static constexpr int WPW = (NIW + NWAVES - 1) / NWAVES;  // weight instructions per wave per step
+    // LDS images are piece planes (structure of arrays): plane q holds piece q
+    // of every record, 16 B per record, planes 256-B aligned.  A wave's
+    // fragment read then touches 16 consecutive records of one plane per
+    // 16-lane group: conflict free for ds_read_b128 with linear addresses.
+    static constexpr int NPIX = (HR * HC + 15) / 16 * 16;       // halo records per plane
+    static constexpr int HPL = NPIX * 16;                        // halo plane bytes
+    static constexpr int NIH = (P * HPL + 1023) / 1024;          // halo DMA wave-instructions
+    static constexpr int HB = NIH * 1024;                        // bytes per halo buffer
+    static constexpr int WPL = BM * 16;                          // weight plane bytes (2 KB)
+    static constexpr int WB1 = P * WPL;                          // weight bytes per tap (8 KB)
+    static constexpr int NIW1 = WB1 / 1024;                      // weight DMA instructions per tap
+    static constexpr bool fits(int tps, int nwb) { return 2 * HB + nwb * tps * WB1 <= 160 * 1024; }
+    // taps per barrier step and weight buffers (DMA lookahead NWB-1 steps)
+    static constexpr int TPS = T == 1 ? 1 : (fits(3, 2) ? 3 : fits(2, 2) ? 2 : 1);
+    static constexpr int NWB = fits(TPS, 3) ? 3 : 2;
+    static constexpr int SPC = (T + TPS - 1) / TPS;           // steps per chunk
+    static constexpr int WB = TPS * WB1;                      // bytes per weight buffer
+    static constexpr int NIWS = TPS * NIW1;                   // weight instructions per full step
+    static constexpr int WPW = (NIWS + NWAVES - 1) / NWAVES;  // ... per wave
+    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;   // halo instructions per wave per chunk
+    static constexpr int Q = (MPW + SPC - 1) / SPC;           // ... issued per step
     static constexpr size_t LDS = 2 * (size_t)HB + NWB * (size_t)WB;
+    static_assert(fits(TPS, NWB), "LDS");
+    static_assert(NIW1 * 1024 == WB1, "whole weight instructions per tap");
 };
 
 template <int KS, int PREC, int EPI>
@@ -170,13 +184,14 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     typedef Prec<PREC> PR;
     typedef typename PR::V V;
     typedef Geo<KS> G;
-    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH, NIW = G::NIW;
-    constexpr int HB = G::HB, WB = G::WB, NWB = G::NWB, WPW = G::WPW;
+    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH, NIW1 = G::NIW1;
+    constexpr int HB = G::HB, WB = G::WB, WB1 = G::WB1, NWB = G::NWB, WPW = G::WPW;
+    constexpr int TPS = G::TPS, SPC = G::SPC, HPL = G::HPL, WPL = G::WPL, NPIX = G::NPIX;
     constexpr int D = NWB - 1;  // weight DMA lookahead (steps)
     constexpr int TERMS = PR::TERMS;
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    char *Hs = lds;           // [2][HB]   halo records [HR][HC][80 B]
-    char *Ws = lds + 2 * HB;  // [NWB][WB] weight records [BM][80 B]
+    char *Hs = lds;           // [2][P planes][NPIX records][16 B]  activation halo
+    char *Ws = lds + 2 * HB;  // [NWB][TPS taps][P planes][BM][16 B] weights
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -197,27 +212,24 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int img = a.unit_image ? a.unit_image[u] : u;
     const int NC = a.NC0 + a.NC1;
 
-    // Per-lane DMA sources (chunk invariant).  LDS piece e of an image is
-    // record e / 5, slot e % 5; slot 4 is the pad (it re-reads piece 0 of
-    // the same 64-B line, no extra traffic) and pieces past the image land in
-    // the buffer's tail.
+    // Per-lane DMA sources (chunk invariant): LDS piece e of the halo image is
+    // plane e / NPIX, record e % NPIX; pad records re-read a legal address.
     int hoff[MPW];
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
-        const int i = wave + NWAVES * m;
-        int e = i * 64 + lane;
-        if (e >= G::NPH) e = 0;
-        const int p = e / LP, q = e % LP;
+        const int e = (wave + NWAVES * m) * 64 + lane;
+        int q = e / NPIX, p = e % NPIX;
+        if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
-        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + (q < P ? q : 0) * 16;
+        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + q * 16;
     }
+    // weight instruction i of a step: tap i / NIW1, plane / channel from i % NIW1
     int woff[WPW];
 #pragma unroll
     for (int m = 0; m < WPW; ++m) {
-        int e = (wave + NWAVES * m) * 64 + lane;
-        if (e >= BM * LP) e = 0;
-        const int n = e / LP, q = e % LP;
-        woff[m] = n * REC + (q < P ? q : 0) * 16;
+        const int e = ((wave + NWAVES * m) % NIW1) * 64 + lane;
+        const int q = e / BM, n = e % BM;
+        woff[m] = n * REC + q * 16;
     }
     const size_t cstride = (size_t)a.Hp * a.Wp * REC;
     auto chunk_src = [&](int c) -> const char * {
@@ -241,19 +253,21 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         return n;
     };
     const char *wsrc0 = a.wp + (size_t)nt * BM * REC;
-    // weight buffer of step s = c*T + tap (compile-time when NWB divides T)
-    auto wbuf = [&](int s, int tap) -> int { return T % NWB == 0 ? tap % NWB : s % NWB; };
-    auto w_dma = [&](int s) -> int {
-        const int c = s / T, tap = s - c * T;
-        const char *src = wsrc0 + ((size_t)tap * NC + c) * (size_t)a.Npad * REC;
-        char *dst = Ws + wbuf(s, tap) * WB;
+    const size_t tapstride = (size_t)NC * a.Npad * REC;
+    // weights of flat step g (chunk g / SPC, taps TPS*(g % SPC) ...); returns the count
+    auto w_dma = [&](int g) -> int {
+        const int c = g / SPC, t0 = (g - c * SPC) * TPS;
+        const int ni = min(TPS, T - t0) * NIW1;
+        const char *src = wsrc0 + (size_t)t0 * tapstride + (size_t)c * a.Npad * REC;
+        char *dst = Ws + (g % NWB) * WB;
         int n = 0;
 #pragma unroll
         for (int m = 0; m < WPW; ++m) {
             const int i = wave + NWAVES * m;
-            if (i < NIW) {
-                __builtin_amdgcn_global_load_lds((const void *)(src + woff[m]),
-                                                 (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+            if (i < ni) {
+                __builtin_amdgcn_global_load_lds(
+                    (const void *)(src + (size_t)(i / NIW1) * tapstride + woff[m]),
+                    (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
                 ++n;
             }
         }
@@ -296,58 +310,62 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     //   F16X3: v0 = [wh|wl] x [xh|xh] (ch 0-7), v1 = same ch 8-15,
     //          v2 = [wh g0|wh g1] x [xl g0|xl g1]
     //   one term: v0 = ch 0-15, v1 = ch 16-31
-    // 80-B records: any 16 consecutive records hit 16 distinct 4-bank groups,
-    // so every ds_read_b128 below is conflict free with linear addresses and
-    // all per-step offsets fold into the instruction's immediate.
+    // (piece planes: linear, conflict-free addresses; per-tap offsets fold
+    // into the ds_read immediate)
     int aoff[TERMS], boff[TERMS];
 #pragma unroll
     for (int v = 0; v < TERMS; ++v) {
         const int aq = TERMS == 3 ? (v == 0 ? 2 * h : v == 1 ? 2 * h + 1 : h) : 2 * v + h;
         const int bqv = TERMS == 3 ? (v == 0 ? 0 : v == 1 ? 1 : 2 + h) : 2 * v + h;
-        aoff[v] = (wn * 64 + l32) * LREC + aq * 16;
-        boff[v] = (wpix * 4 * HC + l32) * LREC + bqv * 16;
+        aoff[v] = aq * WPL + (wn * 64 + l32) * 16;
+        boff[v] = bqv * HPL + (wpix * 4 * HC + l32) * 16;
     }
 
-    const int S = NC * T;
+    const int S = NC * SPC;  // barrier steps
     halo_dma(0, 0, MPW);
-    for (int s0 = 0; s0 < D && s0 < S; ++s0) w_dma(s0);
+    for (int g0 = 0; g0 < D && g0 < S; ++g0) w_dma(g0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
         const char *hl = Hs + (c & 1) * HB;
 #pragma unroll
-        for (int tap = 0; tap < T; ++tap) {
-            const int s = c * T + tap;
-            const int ky = tap / KS, kx = tap % KS;
+        for (int sg = 0; sg < SPC; ++sg) {
+            const int g = c * SPC + sg;
             // DMAs for later steps: halo of chunk c+1 (buffer last read in
-            // chunk c-1), then the weights of step s+D (last read in s-1)
-            const int nh = (c + 1 < NC && tap * Q < MPW) ? halo_dma(c + 1, tap * Q, tap * Q + Q) : 0;
-            const int nw = s + D < S ? w_dma(s + D) : 0;
-            const char *wl = Ws + wbuf(s, tap) * WB;
-            V af[2][TERMS];
+            // chunk c-1), then the weights of step g+D (buffer last read in g-1)
+            const int nh = (c + 1 < NC && sg * Q < MPW) ? halo_dma(c + 1, sg * Q, sg * Q + Q) : 0;
+            const int nw = g + D < S ? w_dma(g + D) : 0;
+            const char *wl = Ws + (g % NWB) * WB;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int tl = 0; tl < TPS; ++tl) {
+                const int tap = sg * TPS + tl;
+                if (tap >= T) break;
+                const int ky = tap / KS, kx = tap % KS;
+                V af[2][TERMS];
 #pragma unroll
-                for (int v = 0; v < TERMS; ++v)
-                    af[i][v] = *reinterpret_cast<const V *>(wl + aoff[v] + i * 32 * LREC);
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                V bf[TERMS];
+                    for (int v = 0; v < TERMS; ++v)
+                        af[i][v] = *reinterpret_cast<const V *>(wl + tl * WB1 + aoff[v] + i * 32 * 16);
 #pragma unroll
-                for (int v = 0; v < TERMS; ++v)
-                    bf[v] = *reinterpret_cast<const V *>(hl + boff[v] + ((j + ky) * HC + kx) * LREC);
+                for (int j = 0; j < 4; ++j) {
+                    V bf[TERMS];
 #pragma unroll
-                for (int v = 0; v < TERMS; ++v)
+                    for (int v = 0; v < TERMS; ++v)
+                        bf[v] = *reinterpret_cast<const V *>(hl + boff[v] + ((j + ky) * HC + kx) * 16);
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+                    for (int v = 0; v < TERMS; ++v)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+                }
             }
-            // the next step needs W(s+1) and, after a chunk's last tap, the
+            // the next step needs W(g+1) and, after a chunk's last step, the
             // whole halo of chunk c+1: leave only younger DMAs in flight
             // (in-order completion; this step issued halo before weights)
             if (D == 1)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             else
-                wait_vmcnt(tap == T - 1 ? nw : nw + nh);
+                wait_vmcnt(sg == SPC - 1 ? nw : nw + nh);
             __builtin_amdgcn_s_barrier();
         }
     }
