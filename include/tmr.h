@@ -172,6 +172,17 @@ int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stre
 int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec);
 int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
                     const float *xmax, void *out, void *stream);
+/* tmr_split_xpack_up: records of [up2x(f) (upsample) or f; 1 (ones)] from the
+ * SAM features f [S][Cin][Hin][Win] (sizes: tmr_split_xpack_size with
+ * C = Cin + ones at the output resolution).  With tmr_split_fold_proj it
+ * feeds the decoder's fp half without materialising fp: conv(input_proj(x))
+ * = conv'([x; 1]), W'[n][c] = sum_k Wd[n][k] P[k][c], W'[n][Cin] = sum_k
+ * Wd[n][k] b[k] per tap (matching_net.py:27-30,56,63-69), fp64 accumulation;
+ * out [N][Cin+1][ks][ks] from wd [N][Cw][ks][ks] (first Cp channels = fp). */
+int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample, int ones,
+                       int ks, int prec, const float *xmax, void *out, void *stream);
+int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
+                        const float *proj_b, int Cin, float *out, void *stream);
 int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec);
 int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, const float *wmax,
                     void *out, void *stream);

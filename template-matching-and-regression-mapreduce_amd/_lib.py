@@ -67,6 +67,8 @@ SIGNATURES = {
     "tmr_absmax": (_I, [_P, _L, _I, _P, _P]),
     "tmr_split_xpack_size": (_L, [_I, _I, _I, _I, _I, _I]),
     "tmr_split_xpack": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_xpack_up": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_fold_proj": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "tmr_split_wpack_size": (_L, [_I, _I, _I, _I, _I]),
     "tmr_split_wpack": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "tmr_split_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,

@@ -61,30 +61,6 @@ struct ConvArgs {
     int leaky;
 };
 
-// Bilinear x2 (align_corners=False) of a half-resolution plane at output
-// (y, x); the fma nesting reproduces ATen's CPU kernel.
-__device__ __forceinline__ void up_coord(int d, int L, int &i0, int &i1, float &l0, float &l1) {
-    float src = 0.5f * ((float)d + 0.5f) - 0.5f;
-    src = src < 0.0f ? 0.0f : src;
-    int a = (int)src;
-    i0 = a;
-    i1 = a + ((a < L - 1) ? 1 : 0);
-    l1 = src - (float)a;
-    l0 = 1.0f - l1;
-}
-
-__device__ __forceinline__ float up_value(const float *plane, int Hin, int Win, int y, int x) {
-    int y0, y1, x0, x1;
-    float ly0, ly1, lx0, lx1;
-    up_coord(y, Hin, y0, y1, ly0, ly1);
-    up_coord(x, Win, x0, x1, lx0, lx1);
-    float a = plane[y0 * Win + x0], b = plane[y0 * Win + x1];
-    float c = plane[y1 * Win + x0], d = plane[y1 * Win + x1];
-    float top = fmaf(lx0, a, lx1 * b);
-    float bot = fmaf(lx0, c, lx1 * d);
-    return fmaf(ly0, top, ly1 * bot);
-}
-
 template <int KS, bool UPS>
 __device__ __forceinline__ float load_x(const ConvArgs &a, int img, int u, int gc, int y, int x) {
     if (gc >= a.C0 + a.C1 || y < 0 || y >= a.H || x < 0 || x >= a.W) return 0.0f;

@@ -108,12 +108,30 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     }
 }
 
+#ifndef TMR_EXP_MFMA16
 __device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x16 mma(b8 a, b8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+#else  // timing experiment only (wrong results): the same FLOPs as 2 x 16x16x32
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <typename VT>
+__device__ __forceinline__ f32x16 mma(VT a, VT b, f32x16 c) {
+    f32x4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+    if constexpr (sizeof(a[0]) == 2 && __is_same(VT, h8)) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
+    } else {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+    }
+    c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
+    c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
+    return c;
+}
+#endif
 
 // one record: CCH fp32 values -> 4 pieces of 8 x 16-bit
 template <int PREC>
@@ -543,6 +561,74 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, i
     for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
 }
 
+// Records of x' = [up2x(f) (or f); 1] straight from the SAM features
+// f [S][Cin][Hin][Win]: the input of the decoder's fp half folded through
+// input_proj (tmr_split_fold_proj).  The bilinear value is the same fma form
+// as tmr_upsample_proj (ATen's CPU kernel); the constant-1 channel carries the
+// projection bias and is zero in the padding, like the conv's zero padding.
+template <int PREC>
+__global__ void xpack_up_kernel(const float *__restrict__ f, int S, int Cin, int Hin, int Win,
+                                int ups, int ones, int H, int W, int NCc, int Hp, int Wp, int pad,
+                                const float *__restrict__ xmax,
+                                typename Prec<PREC>::V *__restrict__ out) {
+    constexpr int CCH = Prec<PREC>::CCH;
+    const int64_t total = (int64_t)S * NCc * Hp * Wp;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int xp = (int)(i % Wp);
+    int64_t r = i / Wp;
+    const int yp = (int)(r % Hp);
+    r /= Hp;
+    const int c = (int)(r % NCc);
+    const int s = (int)(r / NCc);
+    const int y = yp - pad, xx = xp - pad;
+    const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
+    const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
+    float v[MAXCCH];
+#pragma unroll
+    for (int k = 0; k < MAXCCH; ++k) {
+        const int ch = c * CCH + k;
+        float val = 0.0f;
+        if (k < CCH && in) {
+            if (ch < Cin) {
+                const float *pl = f + ((size_t)s * Cin + ch) * Hin * Win;
+                val = ups ? up_value(pl, Hin, Win, y, xx) : pl[(size_t)y * Win + xx];
+            } else if (ones && ch == Cin) {
+                val = 1.0f;
+            }
+        }
+        v[k] = val;
+    }
+    typename Prec<PREC>::V rec[P];
+    split_record<PREC>(v, sc, rec);
+#pragma unroll
+    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
+}
+
+// Fold the decoder's fp half through input_proj (matching_net.py:27-30,56):
+// conv(proj(x)) = conv'([x; 1]) with W'[n][c][t] = sum_k Wd[n][k][t] P[k][c]
+// (c < Cin) and W'[n][Cin][t] = sum_k Wd[n][k][t] b[k]; fp64 accumulation.
+// wd: [N][Cw][T] (its first Cp input channels are the fp half), P: [Cp][Cin].
+__global__ void fold_proj_kernel(const float *__restrict__ wd, int N, int Cw, int Cp, int T,
+                                 const float *__restrict__ pw, const float *__restrict__ pb,
+                                 int Cin, float *__restrict__ out) {
+    const int64_t total = (int64_t)N * (Cin + 1) * T;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int t = (int)(i % T);
+    const int64_t r = i / T;
+    const int c = (int)(r % (Cin + 1));
+    const int n = (int)(r / (Cin + 1));
+    const float *w = wd + (size_t)n * Cw * T + t;
+    double acc = 0.0;
+    if (c < Cin) {
+        for (int k = 0; k < Cp; ++k) acc += (double)w[(size_t)k * T] * (double)pw[(size_t)k * Cin + c];
+    } else {
+        for (int k = 0; k < Cp; ++k) acc += (double)w[(size_t)k * T] * (double)pb[k];
+    }
+    out[i] = (float)acc;
+}
+
 // w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][64 B]; the src0
 // and src1 channel ranges are padded to whole chunks separately.
 template <int PREC>
@@ -669,6 +755,46 @@ extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int k
                                Wp, ks / 2, xmax, static_cast<h8 *>(out));
             break;
     }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample,
+                                  int ones, int ks, int prec, const float *xmax, void *out,
+                                  void *stream) {
+    TMR_REQUIRE(f && out && S > 0 && Cin > 0 && Hin > 0 && Win > 0 && ks_ok(ks) && prec_ok(prec));
+    TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
+    const int H = upsample ? 2 * Hin : Hin, W = upsample ? 2 * Win : Win;
+    const int C = Cin + (ones ? 1 : 0);
+    const int NCc = (int)tmr_cdiv(C, prec_cch(prec)), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int64_t total = (int64_t)S * NCc * Hp * Wp;
+    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
+    hipStream_t s = tmr_stream(stream);
+    const int u = upsample ? 1 : 0, o = ones ? 1 : 0;
+    switch (prec) {
+        case TMR_PREC_F16X3:
+            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_F16X3>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
+                               o, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+        case TMR_PREC_BF16:
+            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_BF16>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
+                               o, H, W, NCc, Hp, Wp, ks / 2, nullptr, static_cast<b8 *>(out));
+            break;
+        default:
+            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_F16>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
+                               o, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+    }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
+                                   const float *proj_b, int Cin, float *out, void *stream) {
+    TMR_REQUIRE(wd && proj_w && proj_b && out && N > 0 && Cp > 0 && Cw >= Cp && Cin > 0 && ks > 0);
+    const int64_t total = (int64_t)N * (Cin + 1) * ks * ks;
+    hipLaunchKernelGGL(fold_proj_kernel, dim3((unsigned)tmr_cdiv(total, 256)), dim3(256), 0,
+                       tmr_stream(stream), wd, N, Cw, Cp, ks * ks, proj_w, proj_b, Cin, out);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

@@ -153,6 +153,38 @@ def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -
     return out
 
 
+def fold_proj(w: torch.Tensor, cp: int, proj_w: torch.Tensor, proj_b: torch.Tensor) -> torch.Tensor:
+    """Fold the first cp input channels of w [N,Cw,k,k] through the 1x1
+    input_proj (proj_w [cp,Cin,1,1], proj_b [cp]) -> [N, Cin+1, k, k]
+    (tmr_split_fold_proj; the last channel multiplies a constant-1 plane)."""
+    require_gpu(w, "conv weight")
+    w = w.detach().float().contiguous()
+    N, Cw, k, _ = w.shape
+    pw = proj_w.detach().float().reshape(cp, -1).contiguous()
+    pb = proj_b.detach().float().contiguous()
+    cin = pw.shape[1]
+    out = torch.empty((N, cin + 1, k, k), device=w.device, dtype=torch.float32)
+    call("tmr_split_fold_proj", ptr(w), N, Cw, cp, k, ptr(pw), ptr(pb), cin, ptr(out), stream())
+    return out
+
+
+def pack_split_up(f: torch.Tensor, upsample: bool, ks: int, precision: str,
+                  xmax: torch.Tensor) -> torch.Tensor:
+    """SAM features [S,Cin,h,w] -> records of [up2x(f) or f; 1] (tmr_split_xpack_up)."""
+    require_gpu(f, "features")
+    f = f.float().contiguous()
+    S, Cin, Hin, Win = f.shape
+    H, W = (2 * Hin, 2 * Win) if upsample else (Hin, Win)
+    pc = prec_code(precision)
+    n = load().tmr_split_xpack_size(S, Cin + 1, H, W, ks, pc)
+    if n <= 0:
+        raise TMRError(f"unsupported feature shape {tuple(f.shape)}")
+    out = torch.empty(n, device=f.device, dtype=torch.uint8)
+    call("tmr_split_xpack_up", ptr(f), S, Cin, Hin, Win, int(upsample), 1, ks, pc, ptr(xmax),
+         ptr(out), stream())
+    return out
+
+
 def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
                  precision: str = "fp32", packed=None):
     """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the split 16-bit
@@ -211,6 +243,10 @@ class TMREngine:
         # fp32 MFMA, "direct" = implicit GEMM on fp32 MFMA
         self.decoder_algo = "split"
         prec_code(cfg.precision)
+        # split kernel + fusion: run the decoder's fp half on [up2x(f); 1]
+        # with weights folded through input_proj (Cin+1 = 257 instead of 512
+        # input channels; same linear map, fp32-level rounding differences)
+        self.fold_proj = True
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -229,11 +265,13 @@ class TMREngine:
         wp = self._cache.get("proj", [w], lambda: pack_conv(w))
         return wp, b.detach().float().contiguous(), w.shape[0], w.shape[1]
 
-    def _fused_decoders(self, split_c0: int = 0, algo: str = "direct"):
+    def _fused_decoders(self, split_c0: int = 0, algo: str = "direct", fold: bool = False):
         """Layer-0 weights of decoder_b and decoder_o concatenated along N, with
         the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders).
         split_c0 > 0 additionally packs the input-channel halves [:c0] / [c0:]
-        (conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM))."""
+        (conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM)).  fold (split
+        kernel, fusion) replaces the fp half by its fold through input_proj:
+        conv_fp(proj(x)) = conv'([x; 1]) (tmr_split_fold_proj), Cin+1 channels."""
         cfg = self.cfg
         layers = ([self._dec_layers("decoder_b")[0]] if cfg.box_reg else []) + \
             [self._dec_layers("decoder_o")[0]]
@@ -243,6 +281,9 @@ class TMREngine:
             lw, lb = self.P["ltrbs_head.head.0.weight"], self.P["ltrbs_head.head.0.bias"]
             heads += [lw, lb]
         tensors = [t for wb in layers for t in wb] + heads
+        if fold:
+            pw_, pb_ = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
+            tensors += [pw_, pb_]
 
         def build():
             W = torch.cat([w.detach().float() for w, _ in layers], 0).contiguous()
@@ -268,13 +309,25 @@ class TMREngine:
                 pk0 = pack_wino if algo == "wino" else pack_conv
                 pk = lambda w_, c0: pk0(w_)  # noqa: E731
             split = None
+            if fold:
+                # fp half folded through input_proj: [N, Cin+1, k, k]
+                Wf = fold_proj(W, c0_full, pw_, pb_)
+                cf = Wf.shape[1]
+                if split_c0:
+                    split = (pk(Wf, cf), pk(W[:, c0_full:].contiguous(), 0),
+                             torch.zeros(N, device=W.device, dtype=torch.float32))
+                    full = None
+                else:
+                    full = pk(torch.cat([Wf, W[:, c0_full:]], 1).contiguous(), cf)
+                return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
             if split_c0:
                 split = (pk(W[:, :split_c0].contiguous(), split_c0), pk(W[:, split_c0:].contiguous(), 0),
                          torch.zeros(N, device=W.device, dtype=torch.float32))
             full = None if split_c0 else pk(W, c0_full)
             return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
 
-        return self._cache.get(f"fused_dec{split_c0}_{algo}_{cfg.precision}", tensors, build)
+        return self._cache.get(f"fused_dec{split_c0}_{algo}_{cfg.precision}_{int(fold)}", tensors,
+                               build)
 
     def _conv(self, name: str, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool):
         """One nn.Conv2d (+ LeakyReLU) of the general-depth stack on the
@@ -330,8 +383,10 @@ class TMREngine:
              ptr(work) if work is not None else None, stream())
         return out, relu
 
-    def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int]):
-        """Decoders + heads over cat([fp[img(u)], f_TM[u]]) -> o [U,1,H,W], b [U,4,H,W]|None."""
+    def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
+               feats: Optional[torch.Tensor] = None):
+        """Decoders + heads over cat([fp[img(u)], f_TM[u]]) -> o [U,1,H,W], b [U,4,H,W]|None.
+        feats (the SAM features fp was projected from) enables the folded fp half."""
         cfg = self.cfg
         U, C1, H, W = f_tm.shape
         dev = f_tm.device
@@ -349,15 +404,30 @@ class TMREngine:
                 algo = "direct"
             wino, splitk = algo == "wino", algo == "split"
             ks = cfg.decoder_kernel_size
-            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0, algo)
+            fold = splitk and cfg.fusion and self.fold_proj and feats is not None
+            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0, algo, fold)
             if Cw != C0 + C1:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
+            if fold:  # the fp half runs on [up2x(f); 1] with Cin+1 channels
+                C0 = feats.shape[1] + 1
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
             acc0 = None
             C0k = C0
             pc = prec_code(cfg.precision)
-            if splitk:
+            if fold:
+                # records of [up2x(f); 1] (max |.| <= max(max|f|, 1): bilinear
+                # weights are convex); one activation scale per conv launch
+                xmax0 = torch.ones(1, device=dev, dtype=torch.float32)
+                absmax(feats, xmax0)
+                if share:
+                    xmax1 = absmax(f_tm)
+                else:
+                    xmax1 = absmax(f_tm, xmax0)
+                xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0)
+                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
+                C0k = C0
+            elif splitk:
                 # 16-bit operand records; one activation scale per conv launch
                 # (both sources of a virtual concat share it)
                 if share:
@@ -443,7 +513,7 @@ class TMREngine:
             relu = torch.relu(f_tm) if want_aux else None
         else:
             f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux)
-        o, b = self.decode(fp, f_tm, unit_image)
+        o, b = self.decode(fp, f_tm, unit_image, feats)
         return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
 
     # ------------------------------------------------------------ post
