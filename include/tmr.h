@@ -95,11 +95,17 @@ int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *
  * its exemplars.
  * squeeze!=0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and
  * `work` must hold U*C*H*W floats; otherwise out is [U,C,H,W] and work may
- * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79). */
+ * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79).
+ * out_absmax (nullable, device float[TMR_ABSMAX_SLOTS]): the kernel raises
+ * the slots so that max over slots >= max |out| (each workgroup's max goes to
+ * one slot; spreading avoids same-address atomics); reduce them with
+ * tmr_absmax(out_absmax, TMR_ABSMAX_SLOTS, ...) into the split decoder's
+ * activation scale source, with no extra pass over out. */
+#define TMR_ABSMAX_SLOTS 256
 int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
               const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
               const float *scale, int squeeze, float *out, float *relu_out, float *work,
-              void *stream);
+              float *out_absmax, void *stream);
 
 /* ---- (a10+a11+a12) conv stack ---------------------------------------------
  * Implicit-GEMM kxk conv over the virtual channel concat

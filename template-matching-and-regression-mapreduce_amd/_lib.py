@@ -55,7 +55,7 @@ SIGNATURES = {
     "tmr_conv_pack": (_I, [_P, _I, _I, _I, _P, _P]),
     "tmr_upsample_proj": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P]),
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
-    "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
+    "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
     "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
     "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),

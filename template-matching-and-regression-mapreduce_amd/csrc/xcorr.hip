@@ -17,6 +17,7 @@ namespace {
 constexpr int NT = 256;
 constexpr int RY = 4;  // output rows per lane
 constexpr int RX = 4;  // output cols per lane
+constexpr int XSLACK = 16;  // zeroed floats past the last LDS row (16-B row reads over-read)
 
 struct XArgs {
     const float *f;
@@ -27,6 +28,7 @@ struct XArgs {
     float *out;
     float *relu_out;
     float *work;
+    unsigned *out_absmax;  // nullable [TMR_ABSMAX_SLOTS]: slot-wise atomicMax of |out|
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
 };
 
@@ -35,11 +37,15 @@ template <int KW>
 __device__ __forceinline__ void corr_block(const float *xs, int W, int x0, int r0,
                                            const float *__restrict__ tc, int h,
                                            float (&acc)[RY][RX]) {
+    constexpr int NV = (KW + RX - 1 + 3) / 4;  // 16-B LDS reads per row (W % 4 == 0: aligned)
     for (int ii = 0; ii < RY + h - 1; ++ii) {
-        const float *xr = xs + (r0 + ii) * W + x0;
-        float xv[KW + RX - 1];
+        const float4 *xr = reinterpret_cast<const float4 *>(xs + (r0 + ii) * W + x0);
+        float xv[4 * NV];
 #pragma unroll
-        for (int j = 0; j < KW + RX - 1; ++j) xv[j] = xr[j];
+        for (int j = 0; j < NV; ++j) {
+            const float4 v4 = xr[j];
+            xv[4 * j] = v4.x; xv[4 * j + 1] = v4.y; xv[4 * j + 2] = v4.z; xv[4 * j + 3] = v4.w;
+        }
 #pragma unroll
         for (int r = 0; r < RY; ++r) {
             const int i = ii - r;
@@ -75,6 +81,10 @@ __device__ __forceinline__ void corr_block_any(const float *xs, int W, int x0, i
 
 __device__ void corr_dispatch(int w, const float *xs, int W, int x0, int r0, const float *tc, int h,
                               float (&acc)[RY][RX]) {
+    if (W & 3) {  // rows not 16-B aligned: scalar reads
+        corr_block_any(xs, W, x0, r0, tc, h, w, acc);
+        return;
+    }
     switch (w) {
 #define TMR_W(K) case K: corr_block<K>(xs, W, x0, r0, tc, h, acc); break;
         TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
@@ -84,28 +94,38 @@ __device__ void corr_dispatch(int w, const float *xs, int W, int x0, int r0, con
     }
 }
 
-__global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
+// tmpl / outp are passed as __restrict__ kernel arguments (not only in XArgs)
+// so the compiler can prove the template reads unclobbered and use scalar
+// loads (s_load_dwordx16 rows) for the wave-uniform taps.
+__global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restrict__ tmpl,
+                                                  float *__restrict__ outp) {
     extern __shared__ float xs[];
     const int band = blockIdx.x, c = blockIdx.y, img = blockIdx.z;
     const int H = a.H, W = a.W;
-    const int u_beg = a.img_units[img], u_end = a.img_units[img + 1];
+    // wave-uniform unit range and descriptors (SGPRs): the template taps then
+    // come in by scalar loads and feed the FMAs as scalar operands
+    const int u_beg = __builtin_amdgcn_readfirstlane(a.img_units[img]);
+    const int u_end = __builtin_amdgcn_readfirstlane(a.img_units[img + 1]);
     if (u_beg >= u_end) return;
     const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
     // input rows needed by any unit of this image: [yb0 - hmax/2, yb1 + hmax/2)
     int hmax = 1;
-    for (int u = u_beg; u < u_end; ++u) hmax = max(hmax, a.units[u].ht);
+    for (int u = u_beg; u < u_end; ++u) hmax = max(hmax, __builtin_amdgcn_readfirstlane(a.units[u].ht));
     const int rlo = max(yb0 - hmax / 2, 0), rhi = min(yb1 + hmax / 2, H);
     const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
     const int nld = (rhi - rlo) * W;
     for (int e = threadIdx.x; e < nld; e += NT) xs[e] = fc[(size_t)rlo * W + e];
     // zero the slack rows/cols the 4x4 register blocks may over-read
-    for (int e = nld + threadIdx.x; e < a.LR * W + RX; e += NT) xs[e] = 0.0f;
+    for (int e = nld + threadIdx.x; e < a.LR * W + XSLACK; e += NT) xs[e] = 0.0f;
     __syncthreads();
 
     const size_t plane = (size_t)H * W;
+    float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
-        const tmr_unit_t un = a.units[u];
-        const int h = un.ht, w = un.wt;
+        const tmr_unit_t &un = a.units[u];
+        const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
         const int Ho = H - h + 1, Wo = W - w + 1;
         const int ya = max(yb0, ph), yz = min(yb1, ph + Ho);  // valid output rows in band
@@ -113,7 +133,7 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
         const float sc = a.squeeze ? 1.0f : *a.scale;
         const float denom = (float)(h * w);
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                              : a.out + ((size_t)u * a.C + c) * plane;
+                              : outp + ((size_t)u * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         if (!a.squeeze) {  // zero border of this band
             for (int e = threadIdx.x; e < (yb1 - yb0) * W; e += NT) {
@@ -124,7 +144,7 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
                 }
             }
         }
-        const float *__restrict__ tc = a.tmpl + un.tmpl_offset + (size_t)c * h * w;
+        const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
         const int nbx = (Wo + RX - 1) / RX, nby = (nv + RY - 1) / RY;
         // LDS row of conv row (ya - ph): ya - ph - rlo
         const int rbase = ya - ph - rlo;
@@ -145,9 +165,23 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
                     const size_t o = (size_t)(ya + r0 + r) * W + x0 + q + pw;
                     const float v = (acc[r][q] / denom) * sc;
                     op[o] = v;
+                    vmax = fmaxf(vmax, fabsf(v));
                     if (rp) rp[o] = v > 0.0f ? v : 0.0f;
                 }
             }
+        }
+    }
+    if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
+        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+        __syncthreads();  // xs is free: every unit's reads are done
+        if ((threadIdx.x & 63) == 0) xs[threadIdx.x >> 6] = vmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float m = xs[0];
+            for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, xs[w]);
+            const unsigned slot = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) %
+                                  TMR_ABSMAX_SLOTS;
+            atomicMax(a.out_absmax + slot, __float_as_uint(m));
         }
     }
 }
@@ -155,23 +189,32 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a) {
 // squeeze (template_matching.py:34-35): sum over channels, pad, scale
 __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_unit_t *__restrict__ units,
                                      int U, int C, int H, int W, const float *__restrict__ scale,
-                                     float *__restrict__ out, float *__restrict__ relu_out) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)U * H * W) return;
-    const int u = (int)(i / ((int64_t)H * W));
-    const int p = (int)(i % ((int64_t)H * W));
-    const int y = p / W, x = p % W;
-    const tmr_unit_t un = units[u];
-    const int ph = un.ht / 2, pw = un.wt / 2, Ho = H - un.ht + 1, Wo = W - un.wt + 1;
+                                     float *__restrict__ out, float *__restrict__ relu_out,
+                                     unsigned *__restrict__ out_absmax) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float v = 0.0f;
-    if (y >= ph && y < ph + Ho && x >= pw && x < pw + Wo) {
-        const float *wp = work + (size_t)u * C * H * W + p;
-        float s = 0.0f;
-        for (int c = 0; c < C; ++c) s += wp[(size_t)c * H * W];
-        v = s * *scale;
+    if (i < (int64_t)U * H * W) {  // no early return: whole waves reach the max reduction
+        const int u = (int)(i / ((int64_t)H * W));
+        const int p = (int)(i % ((int64_t)H * W));
+        const int y = p / W, x = p % W;
+        const tmr_unit_t un = units[u];
+        const int ph = un.ht / 2, pw = un.wt / 2, Ho = H - un.ht + 1, Wo = W - un.wt + 1;
+        if (y >= ph && y < ph + Ho && x >= pw && x < pw + Wo) {
+            const float *wp = work + (size_t)u * C * H * W + p;
+            float s = 0.0f;
+            for (int c = 0; c < C; ++c) s += wp[(size_t)c * H * W];
+            v = s * *scale;
+        }
+        out[i] = v;
+        if (relu_out) relu_out[i] = v > 0.0f ? v : 0.0f;
     }
-    out[i] = v;
-    if (relu_out) relu_out[i] = v > 0.0f ? v : 0.0f;
+    if (out_absmax) {
+        float m = fabsf(v);
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        if ((threadIdx.x & 63) == 0)
+            atomicMax(out_absmax + (blockIdx.x * 4 + (threadIdx.x >> 6)) % TMR_ABSMAX_SLOTS,
+                      __float_as_uint(m));
+    }
 }
 
 }  // namespace
@@ -179,7 +222,7 @@ __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_u
 extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
                          const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
                          int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                         float *work, void *stream) {
+                         float *work, float *out_absmax, void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
@@ -196,13 +239,14 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     a.out = out;
     a.relu_out = relu_out;
     a.work = work;
+    a.out_absmax = reinterpret_cast<unsigned *>(out_absmax);
     a.C = C;
     a.H = H;
     a.W = W;
     a.RB = RB;
     a.squeeze = squeeze;
     a.LR = RB + max_ht - 1 + RY;
-    const size_t lds = ((size_t)a.LR * W + RX) * sizeof(float);
+    const size_t lds = ((size_t)a.LR * W + XSLACK) * sizeof(float);
     hipStream_t s = tmr_stream(stream);
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void *)xcorr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -210,12 +254,13 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
         return TMR_E_HIP;
     TMR_REQUIRE(C < 65536 && B < 65536);
     dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
-    hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a);
+    hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
     TMR_CHECK_LAUNCH();
     if (squeeze) {
         int64_t tot = (int64_t)U * H * W;
         hipLaunchKernelGGL(xcorr_squeeze_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, s,
-                           work, units, U, C, H, W, scale, out, relu_out);
+                           work, units, U, C, H, W, scale, out, relu_out,
+                           reinterpret_cast<unsigned *>(out_absmax));
         TMR_CHECK_LAUNCH();
     }
     return TMR_OK;

@@ -19,6 +19,7 @@ MFMA layouts are derived caches, rebuilt when a parameter changes.
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -29,6 +30,7 @@ from . import host
 from ._lib import PREC_CODES, TMRError, call, load, ptr, require_gpu, stream
 
 NHEAD = 5
+ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
 
 
 @dataclass
@@ -247,6 +249,7 @@ class TMREngine:
         # with weights folded through input_proj (Cin+1 = 257 instead of 512
         # input channels; same linear map, fp32-level rounding differences)
         self.fold_proj = True
+        self._absmax_memo: Dict[tuple, tuple] = {}
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -341,16 +344,55 @@ class TMREngine:
         return conv2d(x, w, b, leaky, wp)
 
     # ------------------------------------------------------------ forward
+    def _feat_absmax(self, feats: torch.Tensor) -> torch.Tensor:
+        """max(1, max |feats|) as a device scalar (memoised per tensor): the
+        scale source of the [up2x(f); 1] records (bilinear weights are convex)."""
+        return self._memo_absmax(feats, "feat", lambda: absmax(
+            feats, torch.ones(1, device=feats.device, dtype=torch.float32)))
+
+    def _memo_absmax(self, t: torch.Tensor, tag: str, compute=None):
+        """Device max scalars memoised per tensor OBJECT and version (a freed
+        tensor's address reused by another never hits)."""
+        key = (t.data_ptr(), tag)
+        hit = self._absmax_memo.get(key)
+        if hit is not None and hit[0]() is t and hit[1] == t._version:
+            return hit[2]
+        if compute is None:
+            return None
+        val = compute()
+        self._absmax_memo[key] = (weakref.ref(t), t._version, val)
+        return val
+
     def project(self, feats: torch.Tensor, want_f0: bool = False):
         """fp = input_proj(up2x(feats)) [B,emb,H,W] (+ f0 = up2x(feats))."""
         require_gpu(feats, "features")
         feats = feats.float().contiguous()
         B, Cin, Hin, Win = feats.shape
+        self._absmax_memo = {}
+        up = self.cfg.feature_upsample
+        H, W = (2 * Hin, 2 * Win) if up else (Hin, Win)
+        if self.decoder_algo == "split" and not want_f0:
+            # 1x1 conv on the split kernel (always the fp32-grade 3-term split:
+            # fp feeds the templates and the correlation) from records of
+            # up2x(f) packed straight from the SAM features
+            pw, pb = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
+            N, Cw = pw.shape[0], pw.shape[1]
+            if Cw != Cin:
+                raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
+            wp, wmax = self._cache.get("proj_split", [pw], lambda: pack_split_w(pw, Cin, "fp32"))
+            xmax = self._feat_absmax(feats)
+            n = load().tmr_split_xpack_size(B, Cin, H, W, 1, 0)
+            xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
+            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up), 0, 1, 0, ptr(xmax),
+                 ptr(xp), stream())
+            fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
+            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, H, W, 1, 0, ptr(wp),
+                 ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fp),
+                 stream())
+            return fp, None
         wp, b, N, Cw = self._proj()
         if Cw != Cin:
             raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
-        up = self.cfg.feature_upsample
-        H, W = (2 * Hin, 2 * Win) if up else (Hin, Win)
         fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
         f0 = None
         if want_f0:
@@ -377,10 +419,13 @@ class TMREngine:
         relu = torch.empty_like(out) if want_relu else None
         work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
         scale = self.P["matcher.scale"].detach().float().contiguous()
+        # max |f_TM| fused in the kernel: per-workgroup maxima into 256 slots
+        slots = torch.zeros(ABSMAX_SLOTS, device=dev, dtype=torch.float32)
         call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh, mw,
              ptr(scale),
              int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
-             ptr(work) if work is not None else None, stream())
+             ptr(work) if work is not None else None, ptr(slots), stream())
+        self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 
     def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
@@ -418,12 +463,12 @@ class TMREngine:
             if fold:
                 # records of [up2x(f); 1] (max |.| <= max(max|f|, 1): bilinear
                 # weights are convex); one activation scale per conv launch
-                xmax0 = torch.ones(1, device=dev, dtype=torch.float32)
-                absmax(feats, xmax0)
+                xmax0 = self._feat_absmax(feats)
+                tm_max = self._memo_absmax(f_tm, "ftm", lambda: absmax(f_tm))
                 if share:
-                    xmax1 = absmax(f_tm)
+                    xmax1 = tm_max
                 else:
-                    xmax1 = absmax(f_tm, xmax0)
+                    xmax1 = absmax(tm_max, xmax0.clone())
                 xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0

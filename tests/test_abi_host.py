@@ -47,11 +47,34 @@ def test_size_queries_no_gpu():
     assert L.tmr_nms_work_size(10, 4) > 10 * 36
 
 
+def test_split_size_queries_no_gpu():
+    """Byte sizes of the split-kernel records (include/tmr.h): activations
+    padded to whole 16x32 tiles plus the ks halo, 64-B records of 16 (fp32
+    3-term) or 32 (bf16/f16) channels; weights [ks^2][chunks][ceil(N/128)*128]."""
+    L = tmr_amd.load()
+    assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 0) == 2 * 32 * 130 * 130 * 64
+    assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 1) == 2 * 16 * 130 * 130 * 64
+    assert L.tmr_split_xpack_size(1, 257, 17, 33, 1, 0) == 1 * 17 * 32 * 64 * 64
+    assert L.tmr_split_xpack_size(1, 8, 8, 8, 4, 0) == -1   # even kernel
+    assert L.tmr_split_xpack_size(1, 8, 8, 8, 3, 5) == -1   # unknown precision
+    assert L.tmr_split_wpack_size(2048, 257, 512, 3, 0) == 9 * (17 + 32) * 2048 * 64
+    assert L.tmr_split_wpack_size(100, 0, 40, 5, 2) == 25 * 2 * 128 * 64
+    assert L.tmr_split_wpack_size(8, 0, 0, 3, 0) == -1
+
+
 def test_invalid_arguments_return_codes():
     L = tmr_amd.load()
     assert L.tmr_conv_pack(None, 1, 1, 3, None, None) == -1
-    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None) == -1
+    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None,
+                       None) == -1
     assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0.5, *([None] * 7)) == -1
+    # split conv: bad precision / kernel size / missing scale sources never launch
+    assert L.tmr_split_conv_store(None, 0, None, None, 8, 1, 8, 8, 3, 9, None, None, None, None, 8, 0,
+                                  None, None, None) == -1
+    assert L.tmr_split_conv_heads(None, 0, None, None, 8, 1, 8, 8, 2, 0, None, None, None, None, 8, 1,
+                                  None, None, None, None) == -1
+    assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, None, None) == -1
+    assert L.tmr_absmax(None, 4, 0, None, None) == -1
 
 
 def test_gpu_only_guard():

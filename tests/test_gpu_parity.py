@@ -105,11 +105,13 @@ def test_xcorr_golden(golden):
         scale = torch.ones(1, device=DEV)
         ud = _units_to_device(units, DEV)
         iu = cuda(np.array([0, 1], np.int32))
+        amax = torch.zeros(256, device=DEV)  # TMR_ABSMAX_SLOTS
         call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), ptr(iu), 1, h, w, ptr(scale), sq,
-             ptr(out), ptr(relu), ptr(work) if work is not None else None, stream())
+             ptr(out), ptr(relu), ptr(work) if work is not None else None, ptr(amax), stream())
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert normwise(got, ref) <= TOL, (i, normwise(got, ref))
+        assert amax.max().item() == np.abs(got).max()  # fused |f_TM| max (split decoder scale)
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0))
         # the pad border is exactly zero
         if h > 1:
