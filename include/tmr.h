@@ -170,7 +170,9 @@ int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, co
  * tmr_split_wpack: w [N][C0+C1][ks][ks] -> [ks*ks][ceil(C0/16)+ceil(C1/16)]
  * [ceil(N/128)*128][rec]; the conv's src0 (per image, C0 channels, packed by
  * xpack with S = images) and src1 (per unit, C1) may both be present.
- * Head partials use 128-channel tiles (tmr_heads_reduce tile_n = 128). */
+ * Records: one 64-B record per pixel per 32-channel chunk (F16X3: a hi and a
+ * lo record); weights [ks*ks][chunks][ceil(N/128)*128][128 B (wh, wl) |
+ * 64 B].  Head partials use 128-channel tiles (tmr_heads_reduce tile_n = 128). */
 #define TMR_PREC_F16X3 0
 #define TMR_PREC_BF16 1
 #define TMR_PREC_F16 2
@@ -192,15 +194,22 @@ int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const fl
 int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec);
 int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, const float *wmax,
                     void *out, void *stream);
+/* flags: TMR_SPLIT_TILED_OUT (store only): `out` receives the raw conv result
+ * (no bias / activation) in the kernel's tiled accumulator layout,
+ * tmr_split_acc_size(U, N, H, W) floats; TMR_SPLIT_TILED_INIT: `acc_init` is
+ * in that layout (indexed by unit_image), e.g. the per-image fp half. */
+#define TMR_SPLIT_TILED_OUT 1
+#define TMR_SPLIT_TILED_INIT 2
+int64_t tmr_split_acc_size(int U, int N, int H, int W);
 int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
                          int C1, int U, int H, int W, int ks, int prec, const void *wpack,
                          const float *wmax, const float *xmax, const float *bias, int N,
-                         int leaky, const float *acc_init, float *out, void *stream);
+                         int leaky, const float *acc_init, float *out, int flags, void *stream);
 int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
                          int C1, int U, int H, int W, int ks, int prec, const void *wpack,
                          const float *wmax, const float *xmax, const float *bias, int N,
                          int leaky, const float *headw, const float *acc_init,
-                         float *partials, void *stream);
+                         float *partials, int flags, void *stream);
 
 /* ---- (a14-a16) peak finder + box decode ------------------------------------
  * Get_pred_boxes per unit (utils/TM_utils.py:245-282): p = sigmoid(o) (or o

@@ -75,11 +75,11 @@ def main():
         runs[f"split_{p}_heads"] = (
             lambda p=p, pc=pc: call("tmr_split_conv_heads", None, 0, ptr(ui), ptr(xs[p]), C, U, H, W, 3,
                                     pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1, ptr(hw),
-                                    ptr(acc0), ptr(part), stream()), fl_d, terms)
+                                    ptr(acc0), ptr(part), 2, stream()), fl_d, terms)  # tiled acc0 (engine)
         runs[f"split_{p}_store"] = (
             lambda p=p, pc=pc: call("tmr_split_conv_store", ptr(xs[p]), C, None, None, 0, U, H, W, 3,
                                     pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 0, None,
-                                    ptr(out), stream()), fl_d, terms)
+                                    ptr(out), 1, stream()), fl_d, terms)  # tiled out (engine)
         runs[f"split_{p}_xpack"] = (lambda p=p: pack_split_x(x, 3, p, xmax), 0.0, 0)
     if os.environ.get("KB_ONLY"):
         runs = {k: v for k, v in runs.items() if k in os.environ["KB_ONLY"].split(",")}

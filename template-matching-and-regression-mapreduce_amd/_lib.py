@@ -41,6 +41,7 @@ TEMPLATE_PROTOTYPE = 1
 
 # decoder-conv precision modes of the split 16-bit-MFMA kernel (include/tmr.h)
 PREC_CODES = {"fp32": 0, "bf16": 1, "f16": 2}
+SPLIT_TILED_OUT, SPLIT_TILED_INIT = 1, 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -71,10 +72,11 @@ SIGNATURES = {
     "tmr_split_fold_proj": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "tmr_split_wpack_size": (_L, [_I, _I, _I, _I, _I]),
     "tmr_split_wpack": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_acc_size": (_L, [_I, _I, _I, _I]),
     "tmr_split_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
-                                  _P, _P, _P]),
+                                  _P, _P, _I, _P]),
     "tmr_split_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
-                                  _P, _P, _P, _P]),
+                                  _P, _P, _P, _I, _P]),
     "tmr_peaks_decode": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "tmr_nms_work_size": (_L, [_L, _L]),
     "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),

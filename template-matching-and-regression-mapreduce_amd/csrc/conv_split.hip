@@ -1,5 +1,5 @@
 // Split-precision direct implicit-GEMM kxk convolution on 16-bit MFMA
-// (v_mfma_f32_32x32x16_f16 / _bf16), gfx950.  Same semantics and ABI role as
+// (v_mfma_f32_16x16x32_f16 / _bf16), gfx950.  Same semantics and ABI role as
 // conv_mfma.hip / conv_wino.hip (Decoder_model conv + LeakyReLU, optional
 // fused 1x1 heads; models/regression_head.py:7-8,31,50,
 // models/matching_net.py:63-75).
@@ -9,37 +9,40 @@
 //          hi/lo parts and power-of-two scales s (max |x s| < 2^14), and
 //          x.w ~= (wh xh + wl xh + wh xl) / (s_x s_w), fp32 accumulation.
 //          The dropped wl xl term and the split residuals are ~2^-22
-//          relative: the result keeps the fp32 path's 1e-5 contract at 1/16
-//          of the MFMA cost of f32-input MFMA x 3 terms.
+//          relative: the result keeps the fp32 path's 1e-5 contract.
 //   BF16   one bf16 term (unscaled), fp32 accumulation (config C).
 //   F16    one scaled fp16 term.
-// Every record is four 16-B pieces (64 B): F16X3 holds 16 channels as
-// [hi ch0-7][hi ch8-15][lo ch0-7][lo ch8-15] (3 MFMAs per 32x32 tile per
-// chunk), BF16/F16 hold 32 channels [ch0-7]..[ch24-31] (2 MFMAs).
 //
 // GEMM view: D[n][pixel] = sum_{tap, c} Wt[tap][n][c] X[c][pixel + tap], A =
-// weights (rows n), B = activations (columns = 32 consecutive pixels of one
-// output row), so a 32x32 accumulator register is one 128-B row segment of
-// the NCHW output (coalesced stores / acc_init loads).
+// weights (rows n), B = activations (columns = 16 consecutive pixels of one
+// output row).  K is walked in 32-channel chunks; one 16x16x32 MFMA consumes
+// a whole chunk (lane group g = lane / 16 supplies channels 8g..8g+7).
 //
 // Operands live in HBM in MFMA-ready 16-bit layouts written by the pack
-// kernels below: per channel chunk a pixel (or output channel) is one
-// 64-B record.
-// Activations are zero-padded to whole tiles plus the kxk halo, so the
-// kernel's loads are never masked.
+// kernels below.  Activations: per 32-channel chunk and "half" (F16X3: hi,
+// lo; one-term modes: one half) a 64-B record per pixel, zero-padded to whole
+// tiles plus the kxk halo, so the kernel never masks a load.  Weights: per
+// tap and chunk a record per output channel, [wh ch0-31][wl ch0-31] (128 B,
+// F16X3) or [w ch0-31] (64 B).
+//
+// The F16X3 K loop alternates two half-chunk kinds over the same 32
+// channels: "hi" (halo xh; 2 MFMAs per tile: wh.xh + wl.xh) and "lo" (halo
+// xl; 1 MFMA: wh.xl).  So every MFMA has a full K = 32, no padding, and the
+// hi and lo halos never need LDS at the same time.
 //
 // Block: 512 threads, 128 output channels x 512 pixels (16 rows x 32 cols).
-// Waves 2 (64 n) x 4 (4 rows); a wave owns 2x4 32x32 accumulators (128 regs).
-// K loop: chunk outer, taps inner, up to 3 taps per barrier step.  The 128
-// weight records of step g+D stream into LDS by LDS-DMA (D+1 buffers) while
-// step g computes, and the next chunk's (16+k-1)x(32+k-1) activation halo
-// (2 buffers) streams in spread over the first steps; each step ends with a
-// counted vmcnt (only the DMAs the next step needs) and a raw s_barrier, so
-// loads stay in flight across barriers.
-// In LDS the records are stored as piece planes (structure of arrays), which
-// makes the ds_read_b128 fragment reads bank-conflict free with plain linear
-// addresses (immediate offsets).
+// Waves 2 (64 n) x 4 (4 rows); a wave owns 4 x 8 16x16 accumulators (128
+// regs).  Per barrier step the weight records of step g+D stream into LDS by
+// LDS-DMA while step g computes, and the next half-chunk's (16+k-1)x(32+k-1)
+// halo (2 buffers) streams in spread over the first steps; each step ends
+// with a counted vmcnt (only the DMAs the next step needs) and a raw
+// s_barrier, so loads stay in flight across barriers.  LDS images are piece
+// planes (structure of arrays, 16 B per record per plane): each 16-lane
+// group of a fragment read touches 16 consecutive records of one plane, so
+// the ds_read_b128 reads are bank-conflict free with linear addresses and
+// every per-tap offset folds into the instruction's immediate.
 #include <algorithm>
+#include <type_traits>
 
 #include "tmr_common.h"
 
@@ -47,7 +50,7 @@ namespace {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
 
 constexpr int BM = 128;      // output channels per block
@@ -56,32 +59,33 @@ constexpr int TW = 32;       // output cols per block
 constexpr int NTHREADS = 512;
 constexpr int NWAVES = 8;
 constexpr int NHEAD = 5;
+constexpr int CCH = 32;      // channels per chunk (one MFMA K)
+constexpr int P = 4;         // 16-B pieces per activation record
+constexpr int XREC = 64;     // bytes per activation record
+constexpr int WPL = BM * 16; // bytes per LDS weight plane
 
 template <int PREC> struct Prec;
 template <> struct Prec<TMR_PREC_F16X3> {
-    static constexpr int CCH = 16;   // channels per record
-    static constexpr int TERMS = 3;  // MFMAs per 32x32 tile per chunk
+    static constexpr int HALVES = 2;   // hi, lo half-chunks per chunk
+    static constexpr int WREC = 128;   // [wh][wl] per output channel
     static constexpr bool SCALED = true;
     typedef _Float16 E;
     typedef h8 V;
 };
 template <> struct Prec<TMR_PREC_BF16> {
-    static constexpr int CCH = 32;
-    static constexpr int TERMS = 2;
+    static constexpr int HALVES = 1;
+    static constexpr int WREC = 64;
     static constexpr bool SCALED = false;
     typedef __bf16 E;
     typedef b8 V;
 };
 template <> struct Prec<TMR_PREC_F16> {
-    static constexpr int CCH = 32;
-    static constexpr int TERMS = 2;
+    static constexpr int HALVES = 1;
+    static constexpr int WREC = 64;
     static constexpr bool SCALED = true;
     typedef _Float16 E;
     typedef h8 V;
 };
-constexpr int P = 4;       // 16-B pieces per record in HBM
-constexpr int REC = 64;    // bytes per record in HBM
-constexpr int MAXCCH = 32;
 
 // power-of-two scale with max |x| * s < 2^14 (fp16 max 65504)
 __device__ __forceinline__ float split_scale(const float *m) {
@@ -104,117 +108,98 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
         case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
         case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
         case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     }
 }
 
-#ifndef TMR_EXP_MFMA16
-__device__ __forceinline__ f32x16 mma(h8 a, h8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+// 16-B LDS-DMA through a buffer descriptor.  Kept in a __device__ function:
+// the builtin inside the kernel's (host-device) lambdas makes the host pass
+// silently drop the kernel stubs.
+__device__ __forceinline__ void buffer_lds16(__amdgpu_buffer_rsrc_t r, lds_ptr_t dst, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
 }
-__device__ __forceinline__ f32x16 mma(b8 a, b8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-#else  // timing experiment only (wrong results): the same FLOPs as 2 x 16x16x32
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-template <typename VT>
-__device__ __forceinline__ f32x16 mma(VT a, VT b, f32x16 c) {
-    f32x4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
-    if constexpr (sizeof(a[0]) == 2 && __is_same(VT, h8)) {
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
-    } else {
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
-    }
-    c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
-    c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
-    return c;
-}
-#endif
 
-// one record: CCH fp32 values -> 4 pieces of 8 x 16-bit
+__device__ __forceinline__ f32x4 mma(h8 a, h8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(b8 a, b8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// one 32-channel record: fp32 values -> hi pieces (and lo pieces for F16X3)
 template <int PREC>
-__device__ __forceinline__ void split_record(const float (&v)[MAXCCH], float s,
-                                             typename Prec<PREC>::V (&out)[P]) {
+__device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
+                                             typename Prec<PREC>::V (&hi)[P],
+                                             typename Prec<PREC>::V (&lo)[P]) {
     typedef typename Prec<PREC>::E E;
-    if (Prec<PREC>::TERMS == 3) {
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < P; ++g)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float xs = v[g * 8 + j] * s;
-                const E hi = (E)xs;
-                out[g][j] = hi;
-                out[2 + g][j] = (E)(xs - (float)hi);
-            }
-    } else {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) out[g][j] = (E)(v[g * 8 + j] * s);
-    }
+        for (int j = 0; j < 8; ++j) {
+            const float xs = v[g * 8 + j] * s;
+            const E h = (E)xs;
+            hi[g][j] = h;
+            if (Prec<PREC>::HALVES == 2) lo[g][j] = (E)(xs - (float)h);
+        }
 }
 
 struct SArgs {
-    const char *x0;   // packed src0 [img][NC0][Hp][Wp][rec]
-    const char *x1;   // packed src1 [u][NC1][Hp][Wp][rec]
+    const char *x0;   // packed src0 [img][NC0*HALVES][Hp][Wp][64 B]
+    const char *x1;   // packed src1 [u][NC1*HALVES][Hp][Wp][64 B]
     const int32_t *unit_image;
-    const char *wp;   // packed weights [tap][NC0+NC1][Npad][rec]
+    const char *wp;   // packed weights [tap][NC0+NC1][Npad][WREC]
     const float *wmax, *xmax;
     const float *bias, *headw, *acc_init;
     float *out, *partials;
     int NC0, NC1, U, H, W, N, NT, MT, TXN, Hp, Wp, Npad, leaky;
+    int flags;  // TMR_SPLIT_TILED_OUT / TMR_SPLIT_TILED_INIT
 };
 
-template <int KS>
+template <int KS, int PREC>
 struct Geo {
     static constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
     static constexpr int T = KS * KS;
-    // LDS images are piece planes (structure of arrays): plane q holds piece q
-    // of every record, 16 B per record, planes 256-B aligned.  A wave's
-    // fragment read then touches 16 consecutive records of one plane per
-    // 16-lane group: conflict free for ds_read_b128 with linear addresses.
-    static constexpr int NPIX = (HR * HC + 15) / 16 * 16;       // halo records per plane
-    static constexpr int HPL = NPIX * 16;                        // halo plane bytes
-    static constexpr int NIH = (P * HPL + 1023) / 1024;          // halo DMA wave-instructions
-    static constexpr int HB = NIH * 1024;                        // bytes per halo buffer
-    static constexpr int WPL = BM * 16;                          // weight plane bytes (2 KB)
-    static constexpr int WB1 = P * WPL;                          // weight bytes per tap (8 KB)
-    static constexpr int NIW1 = WB1 / 1024;                      // weight DMA instructions per tap
+    static constexpr int NPIX = (HR * HC + 15) / 16 * 16;     // halo records per plane
+    static constexpr int HPL = NPIX * 16;                      // halo plane bytes (256-B multiple)
+    static constexpr int NIH = (P * HPL + 1023) / 1024;        // halo DMA wave-instructions
+    static constexpr int HB = NIH * 1024;                      // bytes per halo buffer
+    static constexpr int NPLW = Prec<PREC>::WREC / 16;         // weight planes per tap (8 or 4)
+    static constexpr int WB1 = NPLW * WPL;                     // weight bytes per tap
     static constexpr bool fits(int tps, int nwb) { return 2 * HB + nwb * tps * WB1 <= 160 * 1024; }
     // taps per barrier step and weight buffers (DMA lookahead NWB-1 steps)
-    static constexpr int TPS = T == 1 ? 1 : (fits(3, 2) ? 3 : fits(2, 2) ? 2 : 1);
+    static constexpr int TPS = T == 1 ? 1 : fits(3, 2) ? 3 : fits(2, 2) ? 2 : 1;
     static constexpr int NWB = fits(TPS, 3) ? 3 : 2;
-    static constexpr int SPC = (T + TPS - 1) / TPS;           // steps per chunk
-    static constexpr int WB = TPS * WB1;                      // bytes per weight buffer
-    static constexpr int NIWS = TPS * NIW1;                   // weight instructions per full step
-    static constexpr int WPW = (NIWS + NWAVES - 1) / NWAVES;  // ... per wave
-    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;   // halo instructions per wave per chunk
-    static constexpr int Q = (MPW + SPC - 1) / SPC;           // ... issued per step
+    static constexpr int SPC = (T + TPS - 1) / TPS;            // steps per half-chunk
+    static constexpr int WB = TPS * WB1;                       // bytes per weight buffer
+    static constexpr int WPW = (TPS * NPLW * 2 + NWAVES - 1) / NWAVES;  // weight DMAs per wave per step
+    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;    // halo DMAs per wave per half-chunk
+    static constexpr int Q = (MPW + SPC - 1) / SPC;            // ... issued per step
     static constexpr size_t LDS = 2 * (size_t)HB + NWB * (size_t)WB;
     static_assert(fits(TPS, NWB), "LDS");
-    static_assert(NIW1 * 1024 == WB1, "whole weight instructions per tap");
 };
 
 template <int KS, int PREC, int EPI>
 __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     typedef Prec<PREC> PR;
     typedef typename PR::V V;
-    typedef Geo<KS> G;
-    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH, NIW1 = G::NIW1;
+    typedef Geo<KS, PREC> G;
+    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH;
     constexpr int HB = G::HB, WB = G::WB, WB1 = G::WB1, NWB = G::NWB, WPW = G::WPW;
-    constexpr int TPS = G::TPS, SPC = G::SPC, HPL = G::HPL, WPL = G::WPL, NPIX = G::NPIX;
+    constexpr int TPS = G::TPS, SPC = G::SPC, HPL = G::HPL, NPIX = G::NPIX;
+    constexpr int HALVES = PR::HALVES, WREC = PR::WREC;
     constexpr int D = NWB - 1;  // weight DMA lookahead (steps)
-    constexpr int TERMS = PR::TERMS;
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    char *Hs = lds;           // [2][P planes][NPIX records][16 B]  activation halo
-    char *Ws = lds + 2 * HB;  // [NWB][TPS taps][P planes][BM][16 B] weights
+    char *Hs = lds;           // [2][4 planes][NPIX records][16 B]  activation halo
+    char *Ws = lds + 2 * HB;  // [NWB][TPS taps][NPLW planes][BM][16 B] weights
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-    const int l32 = lane & 31, h = lane >> 5;
+    const int l16 = lane & 15, kg = lane >> 4;
     const int wn = wave & 1, wpix = wave >> 1;
 
     // XCD-aware bijective remap (the 8 XCDs take blocks round robin): the NT
@@ -229,9 +214,11 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int ty0 = (mt / a.TXN) * TH, tx0 = (mt % a.TXN) * TW;
     const int img = a.unit_image ? a.unit_image[u] : u;
     const int NC = a.NC0 + a.NC1;
+    const int NHC = NC * HALVES;
 
-    // Per-lane DMA sources (chunk invariant): LDS piece e of the halo image is
-    // plane e / NPIX, record e % NPIX; pad records re-read a legal address.
+    // Per-lane halo DMA sources (half-chunk invariant): LDS piece e of the
+    // halo image is plane e / NPIX, record e % NPIX; pad records re-read a
+    // legal address.
     int hoff[MPW];
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
@@ -239,53 +226,57 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
-        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * REC + q * 16;
+        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * XREC + q * 16;
     }
-    // weight instruction i of a step: tap i / NIW1, plane / channel from i % NIW1
-    int woff[WPW];
-#pragma unroll
-    for (int m = 0; m < WPW; ++m) {
-        const int e = ((wave + NWAVES * m) % NIW1) * 64 + lane;
-        const int q = e / BM, n = e % BM;
-        woff[m] = n * REC + q * 16;
-    }
-    const size_t cstride = (size_t)a.Hp * a.Wp * REC;
-    auto chunk_src = [&](int c) -> const char * {
-        return c < a.NC0 ? a.x0 + ((size_t)img * a.NC0 + c) * cstride
-                         : a.x1 + ((size_t)u * a.NC1 + (c - a.NC0)) * cstride;
-    };
-    // issue this wave's halo instructions m0 <= m < m1 of chunk c; returns the count
-    auto halo_dma = [&](int c, int m0, int m1) -> int {
-        const char *src = chunk_src(c);
-        char *dst = Hs + (c & 1) * HB;
+    // Buffer descriptors (SGPRs) over this block's source slabs and weights:
+    // every DMA is base + uniform soffset + a 32-bit per-lane voffset, so the
+    // loop holds no 64-bit per-lane addresses (and the range check turns any
+    // stray read into zeros instead of a fault).
+    const uint32_t cstride = (uint32_t)a.Hp * a.Wp * XREC;
+    const int h0 = a.NC0 * HALVES, h1 = a.NC1 * HALVES;
+    const __amdgpu_buffer_rsrc_t xr0 = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(h0 ? a.x0 + (size_t)img * h0 * cstride : a.x1), (short)0, h0 * cstride, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr1 = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(h1 ? a.x1 + (size_t)u * h1 * cstride : a.x0), (short)0, h1 * cstride, 0x00020000);
+    // issue this wave's halo instructions m0 <= m < m1 of half-chunk hc; returns the count
+    auto halo_dma = [&](int hc, int m0, int m1) -> int {
+        const bool s0 = hc < h0;
+        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;
+        char *dst = Hs + (hc & 1) * HB;
         int n = 0;
 #pragma unroll
         for (int m = 0; m < MPW; ++m) {
             const int i = wave + NWAVES * m;
             if (m >= m0 && m < m1 && i < NIH) {
-                __builtin_amdgcn_global_load_lds((const void *)(src + hoff[m]),
-                                                 (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+                buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + i * 1024), hoff[m], soff);
                 ++n;
             }
         }
         return n;
     };
-    const char *wsrc0 = a.wp + (size_t)nt * BM * REC;
-    const size_t tapstride = (size_t)NC * a.Npad * REC;
-    // weights of flat step g (chunk g / SPC, taps TPS*(g % SPC) ...); returns the count
+    // weights of flat step g: half-chunk g / SPC (hi: wh and wl planes, lo:
+    // wh only), taps TPS*(g % SPC)...; instruction i of the step = tap i/IPT,
+    // plane (i%IPT)/2, channels 64*((i%IPT)&1) + lane.  Returns the count.
+    const uint32_t tapstride = (uint32_t)NC * a.Npad * WREC;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.wp + (size_t)nt * BM * WREC), (short)0, T * tapstride - nt * BM * WREC, 0x00020000);
+    const int wlane = lane * WREC;
     auto w_dma = [&](int g) -> int {
-        const int c = g / SPC, t0 = (g - c * SPC) * TPS;
-        const int ni = min(TPS, T - t0) * NIW1;
-        const char *src = wsrc0 + (size_t)t0 * tapstride + (size_t)c * a.Npad * REC;
+        const int hc = g / SPC, t0 = (g - hc * SPC) * TPS;
+        const int c = hc / HALVES;
+        const bool lo = HALVES == 2 && (hc & 1);
+        const int ipt = lo ? 8 : G::NPLW * 2;  // instructions per tap
+        const int ni = min(TPS, T - t0) * ipt;
+        const uint32_t src = (uint32_t)t0 * tapstride + (uint32_t)c * a.Npad * WREC;
         char *dst = Ws + (g % NWB) * WB;
         int n = 0;
 #pragma unroll
         for (int m = 0; m < WPW; ++m) {
             const int i = wave + NWAVES * m;
             if (i < ni) {
-                __builtin_amdgcn_global_load_lds(
-                    (const void *)(src + (size_t)(i / NIW1) * tapstride + woff[m]),
-                    (lds_ptr_t)(dst + i * 1024), 16, 0, 0);
+                const int tl = i / ipt, wi = i - tl * ipt;
+                const uint32_t so = src + (uint32_t)tl * tapstride + ((wi & 1) * 64 * WREC + (wi >> 1) * 16);
+                buffer_lds16(wr, (lds_ptr_t)(dst + tl * WB1 + wi * 1024), wlane, so);
                 ++n;
             }
         }
@@ -294,106 +285,143 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 
     // accumulators start at acc_init (scaled into the accumulator's units by
     // the exact power of two s_x s_w); masked elements read a clamped legal
-    // address and are zeroed by a select, never by a branch around the load
+    // address and are zeroed by a select, never by a branch around the load.
+    // 16x16 accumulator: column = pixel l16, row = n 4*kg + r.
     const float sxw = PR::SCALED ? split_scale(a.xmax) * split_scale(a.wmax) : 1.0f;
     const int HW = a.H * a.W;
-    const int x = tx0 + l32;
-    f32x16 acc[2][4];
-    if (a.acc_init) {
+    f32x4 acc[4][8];
+    // tiled acc layout: [slab][nt][mt][wave][in*8+jp][lane][4] fp32, i.e. each
+    // accumulator register set is one contiguous KB per wave (no masking)
+    const size_t tile_off = ((((size_t)img * a.NT + nt) * a.MT + mt) * NWAVES + wave) * (32 * 64 * 4);
+    if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT)) {
+        const f32x4 *ai = reinterpret_cast<const f32x4 *>(a.acc_init + tile_off) + lane;
+#pragma unroll
+        for (int in = 0; in < 4; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp) acc[in][jp] = ai[(in * 8 + jp) * 64] * sxw;
+    } else if (a.acc_init) {
         const float *ai = a.acc_init + (size_t)img * a.N * HW;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int jp = 0; jp < 8; ++jp) {
+            const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+            const bool pin = y < a.H && x < a.W;
+            const int pix = min(y, a.H - 1) * a.W + min(x, a.W - 1);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int y = ty0 + wpix * 4 + j;
-                const bool pin = y < a.H && x < a.W;
-                const int pix = min(y, a.H - 1) * a.W + min(x, a.W - 1);
+            for (int in = 0; in < 4; ++in)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int n = nt * BM + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                for (int r = 0; r < 4; ++r) {
+                    const int n = nt * BM + wn * 64 + in * 16 + 4 * kg + r;
                     const float v = ai[(size_t)min(n, a.N - 1) * HW + pix];
-                    acc[i][j][r] = (pin && n < a.N) ? v * sxw : 0.0f;
+                    acc[in][jp][r] = (pin && n < a.N) ? v * sxw : 0.0f;
                 }
-            }
+        }
     } else {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int in = 0; in < 4; ++in)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+                for (int r = 0; r < 4; ++r) acc[in][jp][r] = 0.0f;
     }
 
-    // fragment pieces: lane half h supplies k = 8h..8h+7 of each MFMA
-    //   F16X3: v0 = [wh|wl] x [xh|xh] (ch 0-7), v1 = same ch 8-15,
-    //          v2 = [wh g0|wh g1] x [xl g0|xl g1]
-    //   one term: v0 = ch 0-15, v1 = ch 16-31
-    // (piece planes: linear, conflict-free addresses; per-tap offsets fold
-    // into the ds_read immediate)
-    int aoff[TERMS], boff[TERMS];
-#pragma unroll
-    for (int v = 0; v < TERMS; ++v) {
-        const int aq = TERMS == 3 ? (v == 0 ? 2 * h : v == 1 ? 2 * h + 1 : h) : 2 * v + h;
-        const int bqv = TERMS == 3 ? (v == 0 ? 0 : v == 1 ? 1 : 2 + h) : 2 * v + h;
-        aoff[v] = aq * WPL + (wn * 64 + l32) * 16;
-        boff[v] = bqv * HPL + (wpix * 4 * HC + l32) * 16;
-    }
+    // fragment bases: lane group kg supplies K = 8kg..8kg+7 (plane kg; the wl
+    // planes follow the wh planes); per-tap offsets are immediates
+    const int aoff = kg * WPL + (wn * 64 + l16) * 16;
+    const int boff = kg * HPL + (wpix * 4 * HC + l16) * 16;
 
-    const int S = NC * SPC;  // barrier steps
+    const int S = NHC * SPC;  // barrier steps
     halo_dma(0, 0, MPW);
     for (int g0 = 0; g0 < D && g0 < S; ++g0) w_dma(g0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
-        const char *hl = Hs + (c & 1) * HB;
+        // one half-chunk; PART is a compile-time constant (F16X3: 0 = hi, 1 = lo)
+        auto half_chunk = [&](auto part_c) {
+            constexpr int part = decltype(part_c)::value;
+            constexpr bool lo = part == 1;  // F16X3 lo half-chunk: wh . xl only
+            const int hc = c * HALVES + part;
+            const char *hl = Hs + (hc & 1) * HB;
 #pragma unroll
-        for (int sg = 0; sg < SPC; ++sg) {
-            const int g = c * SPC + sg;
-            // DMAs for later steps: halo of chunk c+1 (buffer last read in
-            // chunk c-1), then the weights of step g+D (buffer last read in g-1)
-            const int nh = (c + 1 < NC && sg * Q < MPW) ? halo_dma(c + 1, sg * Q, sg * Q + Q) : 0;
-            const int nw = g + D < S ? w_dma(g + D) : 0;
-            const char *wl = Ws + (g % NWB) * WB;
+            for (int sg = 0; sg < SPC; ++sg) {
+                const int g = hc * SPC + sg;
+                // DMAs for later steps: halo of half-chunk hc+1 (buffer last
+                // read in hc-1), then the weights of step g+D (last read in g-1)
+                const int nh = (hc + 1 < NHC && sg * Q < MPW) ? halo_dma(hc + 1, sg * Q, sg * Q + Q) : 0;
+                const int nw = g + D < S ? w_dma(g + D) : 0;
+                const char *wl = Ws + (g % NWB) * WB;
 #pragma unroll
-            for (int tl = 0; tl < TPS; ++tl) {
-                const int tap = sg * TPS + tl;
-                if (tap >= T) break;
-                const int ky = tap / KS, kx = tap % KS;
-                V af[2][TERMS];
+                for (int tl = 0; tl < TPS; ++tl) {
+                    const int tap = sg * TPS + tl;
+                    if (tap >= T) break;
+                    const int ky = tap / KS, kx = tap % KS;
+                    // passes over the pixel tiles: F16X3 hi = wh.xh then wl.xh
+                    // (the xh fragments are read twice: 4 live A fragments
+                    // instead of 8 keep the loop free of spills), lo = wh.xl,
+                    // one-term = w.x.  A 16x16x32 MFMA per (n tile, pixel tile).
+                    constexpr int NPASS = (HALVES == 2 && !lo) ? 2 : 1;
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                    for (int pass = 0; pass < NPASS; ++pass) {
+                        V aw[4];
 #pragma unroll
-                    for (int v = 0; v < TERMS; ++v)
-                        af[i][v] = *reinterpret_cast<const V *>(wl + tl * WB1 + aoff[v] + i * 32 * 16);
+                        for (int in = 0; in < 4; ++in)
+                            aw[in] = *reinterpret_cast<const V *>(wl + tl * WB1 + pass * 4 * WPL + aoff +
+                                                                  in * 16 * 16);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    V bf[TERMS];
+                        for (int jp = 0; jp < 8; ++jp) {
+                            const V bx = *reinterpret_cast<const V *>(
+                                hl + boff + (((jp >> 1) + ky) * HC + kx + (jp & 1) * 16) * 16);
 #pragma unroll
-                    for (int v = 0; v < TERMS; ++v)
-                        bf[v] = *reinterpret_cast<const V *>(hl + boff[v] + ((j + ky) * HC + kx) * 16);
+                            for (int in = 0; in < 4; ++in) acc[in][jp] = mma(aw[in], bx, acc[in][jp]);
+                        }
+                        // pin the interleave: the A fragments and B(0) first,
+                        // then per pixel tile its 4 MFMAs with B(jp+1) read in
+                        // their shadow.  Unconstrained, hipcc hoists later
+                        // fragments and spills inside the loop, and the
+                        // reloads (vmcnt(0)) drain the counted DMA pipeline.
+                        __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
 #pragma unroll
-                    for (int v = 0; v < TERMS; ++v)
-#pragma unroll
-                        for (int i = 0; i < 2; ++i) acc[i][j] = mma(af[i][v], bf[v], acc[i][j]);
+                        for (int jp = 0; jp < 7; ++jp) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
+                // the next step needs W(g+1) and, after a half-chunk's last
+                // step, the whole halo of hc+1: leave only younger DMAs in
+                // flight (in-order completion; halo issued before weights)
+                if (D == 1)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else
+                    wait_vmcnt(sg == SPC - 1 ? nw : nw + nh);
+                __builtin_amdgcn_s_barrier();
             }
-            // the next step needs W(g+1) and, after a chunk's last step, the
-            // whole halo of chunk c+1: leave only younger DMAs in flight
-            // (in-order completion; this step issued halo before weights)
-            if (D == 1)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else
-                wait_vmcnt(sg == SPC - 1 ? nw : nw + nh);
-            __builtin_amdgcn_s_barrier();
-        }
+        };
+        half_chunk(std::integral_constant<int, 0>{});
+        if constexpr (HALVES == 2) half_chunk(std::integral_constant<int, 1>{});
     }
 
     // ---------------- epilogue ----------------
     const float inv = 1.0f / sxw;  // 2^-k: exact
+    if (EPI == 0 && (a.flags & TMR_SPLIT_TILED_OUT)) {
+        // raw conv result (scaled back) in the tiled acc layout of slab u: the
+        // acc_init of a later launch; bias / activation are not applied here
+        f32x4 *o = reinterpret_cast<f32x4 *>(
+                       a.out + ((((size_t)u * a.NT + nt) * a.MT + mt) * NWAVES + wave) * (32 * 64 * 4)) +
+                   lane;
+#pragma unroll
+        for (int in = 0; in < 4; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp) o[(in * 8 + jp) * 64] = acc[in][jp] * inv;
+        return;
+    }
     // the block's bias and head weights through LDS (the main loop's last
     // barrier freed it): global loads here would be hoisted into registers
-    float *sb = reinterpret_cast<float *>(lds) + NHEAD * 16 * 32;  // past the head scratch
-    float *shw = sb + BM;                                           // [BM][NHEAD]
+    float *red = reinterpret_cast<float *>(lds);   // [4 wpix][8 jp][NHEAD][16]
+    float *sb = red + 4 * 8 * NHEAD * 16;
+    float *shw = sb + BM;                          // [BM][NHEAD]
     if (tid < BM) {
         const int n = nt * BM + tid;
         sb[tid] = n < a.N ? a.bias[n] : 0.0f;
@@ -401,16 +429,16 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     if (EPI == 1)
         for (int e = tid; e < BM * NHEAD; e += NTHREADS) shw[e] = a.headw[(size_t)nt * BM * NHEAD + e];
     __syncthreads();
-    float hs[4][NHEAD];
+    float hs[8][NHEAD];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
-        for (int k = 0; k < NHEAD; ++k) hs[j][k] = 0.0f;
+        for (int k = 0; k < NHEAD; ++k) hs[jp][k] = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int in = 0; in < 4; ++in)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int nl = wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        for (int r = 0; r < 4; ++r) {
+            const int nl = wn * 64 + in * 16 + 4 * kg + r;
             const int n = nt * BM + nl;
             const bool nin = n < a.N;
             const float bn = sb[nl];
@@ -420,42 +448,43 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 for (int k = 0; k < NHEAD; ++k) hw[k] = shw[nl * NHEAD + k];
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int y = ty0 + wpix * 4 + j;
-                const bool pin = nin && y < a.H && x < a.W;
-                const size_t pix = (size_t)y * a.W + x;
-                float v = acc[i][j][r] * inv;
-                v += bn;
+            for (int jp = 0; jp < 8; ++jp) {
+                const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+                float v = acc[in][jp][r] * inv + bn;
                 if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
                 if (EPI == 0) {
-                    if (pin) a.out[((size_t)u * a.N + n) * HW + pix] = v;
+                    if (nin && y < a.H && x < a.W) a.out[((size_t)u * a.N + n) * HW + (size_t)y * a.W + x] = v;
                 } else {
 #pragma unroll
-                    for (int k = 0; k < NHEAD; ++k) hs[j][k] = fmaf(v, hw[k], hs[j][k]);
+                    for (int k = 0; k < NHEAD; ++k) hs[jp][k] = fmaf(v, hw[k], hs[jp][k]);
                 }
             }
         }
     if (EPI == 1) {
+        // sum over the 4 lane groups (n rows), then over the two n-waves
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
-            for (int k = 0; k < NHEAD; ++k) hs[j][k] += __shfl_xor(hs[j][k], 32);
-        float *red = reinterpret_cast<float *>(lds);  // [4 wpix][4 j][NHEAD][32]
-        if (wn == 1 && h == 0) {
+            for (int k = 0; k < NHEAD; ++k) {
+                hs[jp][k] += __shfl_xor(hs[jp][k], 16);
+                hs[jp][k] += __shfl_xor(hs[jp][k], 32);
+            }
+        __syncthreads();  // sb / shw reads are done before red is written
+        if (wn == 1 && kg == 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
-                for (int k = 0; k < NHEAD; ++k) red[((wpix * 4 + j) * NHEAD + k) * 32 + l32] = hs[j][k];
+                for (int k = 0; k < NHEAD; ++k) red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16] = hs[jp][k];
         }
         __syncthreads();
-        if (wn == 0 && h == 0 && x < a.W) {
+        if (wn == 0 && kg == 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int y = ty0 + wpix * 4 + j;
-                if (y >= a.H) continue;
+            for (int jp = 0; jp < 8; ++jp) {
+                const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+                if (y >= a.H || x >= a.W) continue;
 #pragma unroll
                 for (int k = 0; k < NHEAD; ++k) {
-                    const float v = hs[j][k] + red[((wpix * 4 + j) * NHEAD + k) * 32 + l32];
+                    const float v = hs[jp][k] + red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16];
                     a.partials[(((size_t)nt * NHEAD + k) * a.U + u) * HW + (size_t)y * a.W + x] = v;
                 }
             }
@@ -465,9 +494,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 
 template <int KS, int PREC, int EPI>
 int launch_split(SArgs a, hipStream_t s) {
-    constexpr size_t lds = Geo<KS>::LDS;
+    constexpr size_t lds = Geo<KS, PREC>::LDS;
     static_assert(lds <= 160 * 1024, "LDS");
-    static_assert((NHEAD * 16 * 32 + BM * (NHEAD + 1)) * 4 <= lds, "epilogue scratch");
+    static_assert((4 * 8 * NHEAD * 16 + BM * (NHEAD + 1)) * 4 <= lds, "epilogue scratch");
     auto kern = split_conv_kernel<KS, PREC, EPI>;
     if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
@@ -501,7 +530,8 @@ int dispatch_ks(int ks, int prec, const SArgs &a, hipStream_t s) {
     }
 }
 
-inline int prec_cch(int prec) { return prec == TMR_PREC_F16X3 ? Prec<TMR_PREC_F16X3>::CCH : Prec<TMR_PREC_BF16>::CCH; }
+inline int prec_halves(int prec) { return prec == TMR_PREC_F16X3 ? 2 : 1; }
+inline int prec_wrec(int prec) { return prec == TMR_PREC_F16X3 ? 128 : 64; }
 inline bool prec_ok(int prec) {
     return prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16;
 }
@@ -530,13 +560,18 @@ __global__ void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4, unsi
     if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// x [S][C][H][W] fp32 -> [S][ceil(C/CCH)][Hp][Wp][64 B], zero padded:
-// padded (yp, xp) holds x[yp - ks/2][xp - ks/2].  One thread per record.
-template <int PREC>
-__global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, int W, int NCc,
-                             int Hp, int Wp, int pad, const float *__restrict__ xmax,
-                             typename Prec<PREC>::V *__restrict__ out) {
-    constexpr int CCH = Prec<PREC>::CCH;
+// Activation records: value v(s, ch, y, x) -> [S][NCc*HALVES][Hp][Wp][64 B],
+// padded (yp, xp) holding v at (yp - ks/2, xp - ks/2), zero outside.  One
+// thread per (s, chunk, yp, xp) writes the chunk's hi (and lo) record.
+// MODE 0: v = x[s][ch][y][x]; MODE 1: v = [up2x(f) or f; 1] from the SAM
+// features (the fp-half fold, tmr_split_fold_proj / the input_proj input):
+// the same fma form as tmr_upsample_proj (ATen's CPU kernel); the constant-1
+// channel carries the projection bias and is zero in the padding.
+template <int PREC, int MODE>
+__global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hin, int Win, int ups,
+                             int ones, int H, int W, int NCc, int Hp, int Wp, int pad,
+                             const float *__restrict__ xmax, typename Prec<PREC>::V *__restrict__ out) {
+    constexpr int HALVES = Prec<PREC>::HALVES;
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
@@ -549,49 +584,16 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int C, int H, i
     const int y = yp - pad, xx = xp - pad;
     const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
     const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
-    float v[MAXCCH];
+    float v[CCH];
 #pragma unroll
-    for (int k = 0; k < MAXCCH; ++k) {
-        const int ch = c * CCH + k;
-        v[k] = (k < CCH && in && ch < C) ? x[(((size_t)s * C + ch) * H + y) * W + xx] : 0.0f;
-    }
-    typename Prec<PREC>::V rec[P];
-    split_record<PREC>(v, sc, rec);
-#pragma unroll
-    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
-}
-
-// Records of x' = [up2x(f) (or f); 1] straight from the SAM features
-// f [S][Cin][Hin][Win]: the input of the decoder's fp half folded through
-// input_proj (tmr_split_fold_proj).  The bilinear value is the same fma form
-// as tmr_upsample_proj (ATen's CPU kernel); the constant-1 channel carries the
-// projection bias and is zero in the padding, like the conv's zero padding.
-template <int PREC>
-__global__ void xpack_up_kernel(const float *__restrict__ f, int S, int Cin, int Hin, int Win,
-                                int ups, int ones, int H, int W, int NCc, int Hp, int Wp, int pad,
-                                const float *__restrict__ xmax,
-                                typename Prec<PREC>::V *__restrict__ out) {
-    constexpr int CCH = Prec<PREC>::CCH;
-    const int64_t total = (int64_t)S * NCc * Hp * Wp;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int xp = (int)(i % Wp);
-    int64_t r = i / Wp;
-    const int yp = (int)(r % Hp);
-    r /= Hp;
-    const int c = (int)(r % NCc);
-    const int s = (int)(r / NCc);
-    const int y = yp - pad, xx = xp - pad;
-    const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
-    const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
-    float v[MAXCCH];
-#pragma unroll
-    for (int k = 0; k < MAXCCH; ++k) {
+    for (int k = 0; k < CCH; ++k) {
         const int ch = c * CCH + k;
         float val = 0.0f;
-        if (k < CCH && in) {
-            if (ch < Cin) {
-                const float *pl = f + ((size_t)s * Cin + ch) * Hin * Win;
+        if (in) {
+            if (MODE == 0) {
+                if (ch < Cin) val = x[(((size_t)s * Cin + ch) * H + y) * W + xx];
+            } else if (ch < Cin) {
+                const float *pl = x + ((size_t)s * Cin + ch) * Hin * Win;
                 val = ups ? up_value(pl, Hin, Win, y, xx) : pl[(size_t)y * Win + xx];
             } else if (ones && ch == Cin) {
                 val = 1.0f;
@@ -599,10 +601,16 @@ __global__ void xpack_up_kernel(const float *__restrict__ f, int S, int Cin, int
         }
         v[k] = val;
     }
-    typename Prec<PREC>::V rec[P];
-    split_record<PREC>(v, sc, rec);
+    typename Prec<PREC>::V hi[P], lo[P];
+    split_record<PREC>(v, sc, hi, lo);
+    const size_t plane = (size_t)Hp * Wp;
+    typename Prec<PREC>::V *o = out + (((size_t)s * NCc + c) * HALVES * plane + (size_t)yp * Wp + xp) * P;
 #pragma unroll
-    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
+    for (int q = 0; q < P; ++q) o[q] = hi[q];
+    if (HALVES == 2) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) o[plane * P + q] = lo[q];
+    }
 }
 
 // Fold the decoder's fp half through input_proj (matching_net.py:27-30,56):
@@ -629,13 +637,12 @@ __global__ void fold_proj_kernel(const float *__restrict__ wd, int N, int Cw, in
     out[i] = (float)acc;
 }
 
-// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][64 B]; the src0
-// and src1 channel ranges are padded to whole chunks separately.
+// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][WREC]; the src0
+// and src1 channel ranges are padded to whole 32-channel chunks separately.
 template <int PREC>
 __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1, int ks, int NC0,
                              int NC, int Npad, const float *__restrict__ wmax,
                              typename Prec<PREC>::V *__restrict__ out) {
-    constexpr int CCH = Prec<PREC>::CCH;
     const int T = ks * ks;
     const int64_t total = (int64_t)T * NC * Npad;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -646,15 +653,12 @@ __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1,
     const int tap = (int)(r / NC);
     const int C = C0 + C1;
     const float sc = Prec<PREC>::SCALED ? split_scale(wmax) : 1.0f;
-    float v[MAXCCH];
+    float v[CCH];
 #pragma unroll
-    for (int k = 0; k < MAXCCH; ++k) {
+    for (int k = 0; k < CCH; ++k) {
         int ch;
         bool ok;
-        if (k >= CCH) {
-            ch = 0;
-            ok = false;
-        } else if (c < NC0) {
+        if (c < NC0) {
             ch = c * CCH + k;
             ok = ch < C0;
         } else {
@@ -664,16 +668,22 @@ __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1,
         }
         v[k] = (ok && n < N) ? w[((size_t)n * C + ch) * T + tap] : 0.0f;
     }
-    typename Prec<PREC>::V rec[P];
-    split_record<PREC>(v, sc, rec);
+    typename Prec<PREC>::V hi[P], lo[P];
+    split_record<PREC>(v, sc, hi, lo);
+    constexpr int NP = Prec<PREC>::WREC / 16;
+    typename Prec<PREC>::V *o = out + i * NP;
 #pragma unroll
-    for (int q = 0; q < P; ++q) out[i * P + q] = rec[q];
+    for (int q = 0; q < P; ++q) o[q] = hi[q];
+    if (NP == 8) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) o[P + q] = lo[q];
+    }
 }
 
 int split_common(const void *xp0, int C0, const int32_t *unit_image, const void *xp1, int C1, int U,
                  int H, int W, int ks, int prec, const void *wpack, const float *wmax,
                  const float *xmax, const float *bias, int N, int leaky, const float *acc_init,
-                 float *out, const float *headw, float *partials, int epi, void *stream) {
+                 float *out, const float *headw, float *partials, int epi, int flags, void *stream) {
     TMR_REQUIRE(prec_ok(prec) && ks_ok(ks));
     TMR_REQUIRE(wpack && bias && U > 0 && H > 0 && W > 0 && N > 0 && C0 >= 0 && C1 >= 0);
     TMR_REQUIRE(C0 + C1 > 0 && (C0 == 0 || xp0) && (C1 == 0 || xp1));
@@ -690,8 +700,8 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     a.acc_init = acc_init;
     a.out = out;
     a.partials = partials;
-    a.NC0 = (int)tmr_cdiv(C0, prec_cch(prec));
-    a.NC1 = (int)tmr_cdiv(C1, prec_cch(prec));
+    a.NC0 = (int)tmr_cdiv(C0, CCH);
+    a.NC1 = (int)tmr_cdiv(C1, CCH);
     a.U = U;
     a.H = H;
     a.W = W;
@@ -703,8 +713,35 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     a.Hp = pad_h(H, ks);
     a.Wp = pad_w(W, ks);
     a.leaky = leaky;
+    a.flags = flags;
     hipStream_t s = tmr_stream(stream);
     return epi ? dispatch_ks<1>(ks, prec, a, s) : dispatch_ks<0>(ks, prec, a, s);
+}
+
+template <int MODE>
+int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int ones, int H, int W,
+                 int ks, int prec, const float *xmax, void *out, void *stream) {
+    const int C = Cin + (MODE == 1 && ones ? 1 : 0);
+    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int64_t total = (int64_t)S * NCc * Hp * Wp;
+    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
+    hipStream_t s = tmr_stream(stream);
+    switch (prec) {
+        case TMR_PREC_F16X3:
+            hipLaunchKernelGGL((xpack_kernel<TMR_PREC_F16X3, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+        case TMR_PREC_BF16:
+            hipLaunchKernelGGL((xpack_kernel<TMR_PREC_BF16, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, nullptr, static_cast<b8 *>(out));
+            break;
+        default:
+            hipLaunchKernelGGL((xpack_kernel<TMR_PREC_F16, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+            break;
+    }
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
 }
 
 }  // namespace
@@ -730,33 +767,14 @@ extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out,
 
 extern "C" int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec) {
     if (S <= 0 || C <= 0 || H <= 0 || W <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
-    return (int64_t)S * tmr_cdiv(C, prec_cch(prec)) * pad_h(H, ks) * pad_w(W, ks) * REC;
+    return (int64_t)S * tmr_cdiv(C, CCH) * prec_halves(prec) * pad_h(H, ks) * pad_w(W, ks) * XREC;
 }
 
 extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
                                const float *xmax, void *out, void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
-    const int NCc = (int)tmr_cdiv(C, prec_cch(prec)), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
-    const int64_t total = (int64_t)S * NCc * Hp * Wp;
-    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
-    hipStream_t s = tmr_stream(stream);
-    switch (prec) {
-        case TMR_PREC_F16X3:
-            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_F16X3>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
-                               Wp, ks / 2, xmax, static_cast<h8 *>(out));
-            break;
-        case TMR_PREC_BF16:
-            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_BF16>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
-                               Wp, ks / 2, nullptr, static_cast<b8 *>(out));
-            break;
-        default:
-            hipLaunchKernelGGL(xpack_kernel<TMR_PREC_F16>, grid, blk, 0, s, x, S, C, H, W, NCc, Hp,
-                               Wp, ks / 2, xmax, static_cast<h8 *>(out));
-            break;
-    }
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
+    return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, out, stream);
 }
 
 extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample,
@@ -765,28 +783,8 @@ extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int W
     TMR_REQUIRE(f && out && S > 0 && Cin > 0 && Hin > 0 && Win > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
     const int H = upsample ? 2 * Hin : Hin, W = upsample ? 2 * Win : Win;
-    const int C = Cin + (ones ? 1 : 0);
-    const int NCc = (int)tmr_cdiv(C, prec_cch(prec)), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
-    const int64_t total = (int64_t)S * NCc * Hp * Wp;
-    const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
-    hipStream_t s = tmr_stream(stream);
-    const int u = upsample ? 1 : 0, o = ones ? 1 : 0;
-    switch (prec) {
-        case TMR_PREC_F16X3:
-            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_F16X3>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
-                               o, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
-            break;
-        case TMR_PREC_BF16:
-            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_BF16>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
-                               o, H, W, NCc, Hp, Wp, ks / 2, nullptr, static_cast<b8 *>(out));
-            break;
-        default:
-            hipLaunchKernelGGL(xpack_up_kernel<TMR_PREC_F16>, grid, blk, 0, s, f, S, Cin, Hin, Win, u,
-                               o, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
-            break;
-    }
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
+    return xpack_launch<1>(f, S, Cin, Hin, Win, upsample ? 1 : 0, ones ? 1 : 0, H, W, ks, prec, xmax,
+                           out, stream);
 }
 
 extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
@@ -799,18 +797,22 @@ extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int k
     return TMR_OK;
 }
 
+extern "C" int64_t tmr_split_acc_size(int U, int N, int H, int W) {
+    if (U <= 0 || N <= 0 || H <= 0 || W <= 0) return -1;
+    return (int64_t)U * tmr_cdiv(N, BM) * BM * tmr_cdiv(H, TH) * TH * tmr_cdiv(W, TW) * TW;
+}
+
 extern "C" int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec) {
     if (N <= 0 || C0 < 0 || C1 < 0 || C0 + C1 <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
-    const int cc = prec_cch(prec);
-    return (int64_t)ks * ks * (tmr_cdiv(C0, cc) + tmr_cdiv(C1, cc)) * tmr_cdiv(N, BM) * BM * REC;
+    return (int64_t)ks * ks * (tmr_cdiv(C0, CCH) + tmr_cdiv(C1, CCH)) * tmr_cdiv(N, BM) * BM *
+           prec_wrec(prec);
 }
 
 extern "C" int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec,
                                const float *wmax, void *out, void *stream) {
     TMR_REQUIRE(w && out && N > 0 && C0 >= 0 && C1 >= 0 && C0 + C1 > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || wmax);
-    const int cc = prec_cch(prec);
-    const int NC0 = (int)tmr_cdiv(C0, cc), NC = NC0 + (int)tmr_cdiv(C1, cc);
+    const int NC0 = (int)tmr_cdiv(C0, CCH), NC = NC0 + (int)tmr_cdiv(C1, CCH);
     const int Npad = (int)tmr_cdiv(N, BM) * BM;
     const int64_t total = (int64_t)ks * ks * NC * Npad;
     const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
@@ -837,18 +839,19 @@ extern "C" int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit
                                     const void *xp1, int C1, int U, int H, int W, int ks, int prec,
                                     const void *wpack, const float *wmax, const float *xmax,
                                     const float *bias, int N, int leaky, const float *acc_init,
-                                    float *out, void *stream) {
+                                    float *out, int flags, void *stream) {
     TMR_REQUIRE(out);
     return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
-                        leaky, acc_init, out, nullptr, nullptr, 0, stream);
+                        leaky, acc_init, out, nullptr, nullptr, 0, flags, stream);
 }
 
 extern "C" int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image,
                                     const void *xp1, int C1, int U, int H, int W, int ks, int prec,
                                     const void *wpack, const float *wmax, const float *xmax,
                                     const float *bias, int N, int leaky, const float *headw,
-                                    const float *acc_init, float *partials, void *stream) {
-    TMR_REQUIRE(headw && partials);
+                                    const float *acc_init, float *partials, int flags,
+                                    void *stream) {
+    TMR_REQUIRE(headw && partials && !(flags & TMR_SPLIT_TILED_OUT));
     return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
-                        leaky, acc_init, nullptr, headw, partials, 1, stream);
+                        leaky, acc_init, nullptr, headw, partials, 1, flags, stream);
 }

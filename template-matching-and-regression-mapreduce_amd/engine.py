@@ -27,7 +27,8 @@ import numpy as np
 import torch
 
 from . import host
-from ._lib import PREC_CODES, TMRError, call, load, ptr, require_gpu, stream
+from ._lib import (PREC_CODES, SPLIT_TILED_INIT, SPLIT_TILED_OUT, TMRError, call, load, ptr,
+                   require_gpu, stream)
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
@@ -203,7 +204,7 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
     call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, prec_code(precision),
          ptr(wp), ptr(wmax), ptr(xmax), ptr(b.detach().float().contiguous()), N, int(leaky), None,
-         ptr(out), stream())
+         ptr(out), 0, stream())
     return out
 
 
@@ -388,7 +389,7 @@ class TMREngine:
             fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
             call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, H, W, 1, 0, ptr(wp),
                  ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fp),
-                 stream())
+                 0, stream())
             return fp, None
         wp, b, N, Cw = self._proj()
         if Cw != Cin:
@@ -486,11 +487,16 @@ class TMREngine:
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
             if share:
                 wp_fp, wp_tm, zero_b = split
-                acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
-                if splitk:
+                if splitk:  # acc0 in the kernel's tiled accumulator layout (private)
+                    acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
+                                       dtype=torch.float32)
                     call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
                          ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0, None,
-                         ptr(acc0), stream())
+                         ptr(acc0), SPLIT_TILED_OUT, stream())
+                else:
+                    acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
+                if splitk:
+                    pass  # launched above
                 elif wino:
                     call("tmr_wino_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
                          ptr(zero_b), N, 0, None, ptr(acc0), stream())
@@ -507,7 +513,7 @@ class TMREngine:
             if splitk:
                 call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                      U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
-                     a0, ptr(part), stream())
+                     a0, ptr(part), SPLIT_TILED_INIT if a0 is not None else 0, stream())
             elif wino:
                 call("tmr_wino_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
                      ptr(bias), N, 1, ptr(hw), a0, ptr(part), stream())

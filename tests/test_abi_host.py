@@ -49,15 +49,16 @@ def test_size_queries_no_gpu():
 
 def test_split_size_queries_no_gpu():
     """Byte sizes of the split-kernel records (include/tmr.h): activations
-    padded to whole 16x32 tiles plus the ks halo, 64-B records of 16 (fp32
-    3-term) or 32 (bf16/f16) channels; weights [ks^2][chunks][ceil(N/128)*128]."""
+    padded to whole 16x32 tiles plus the ks halo, one 64-B record per pixel per
+    32-channel chunk and half (fp32 3-term: hi and lo halves); weights
+    [ks^2][chunks][ceil(N/128)*128][128 B (wh, wl) | 64 B]."""
     L = tmr_amd.load()
     assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 0) == 2 * 32 * 130 * 130 * 64
     assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 1) == 2 * 16 * 130 * 130 * 64
-    assert L.tmr_split_xpack_size(1, 257, 17, 33, 1, 0) == 1 * 17 * 32 * 64 * 64
+    assert L.tmr_split_xpack_size(1, 257, 17, 33, 1, 0) == 1 * 9 * 2 * 32 * 64 * 64
     assert L.tmr_split_xpack_size(1, 8, 8, 8, 4, 0) == -1   # even kernel
     assert L.tmr_split_xpack_size(1, 8, 8, 8, 3, 5) == -1   # unknown precision
-    assert L.tmr_split_wpack_size(2048, 257, 512, 3, 0) == 9 * (17 + 32) * 2048 * 64
+    assert L.tmr_split_wpack_size(2048, 257, 512, 3, 0) == 9 * (9 + 16) * 2048 * 128
     assert L.tmr_split_wpack_size(100, 0, 40, 5, 2) == 25 * 2 * 128 * 64
     assert L.tmr_split_wpack_size(8, 0, 0, 3, 0) == -1
 
@@ -70,9 +71,11 @@ def test_invalid_arguments_return_codes():
     assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0.5, *([None] * 7)) == -1
     # split conv: bad precision / kernel size / missing scale sources never launch
     assert L.tmr_split_conv_store(None, 0, None, None, 8, 1, 8, 8, 3, 9, None, None, None, None, 8, 0,
-                                  None, None, None) == -1
+                                  None, None, 0, None) == -1
     assert L.tmr_split_conv_heads(None, 0, None, None, 8, 1, 8, 8, 2, 0, None, None, None, None, 8, 1,
-                                  None, None, None, None) == -1
+                                  None, None, None, 0, None) == -1
+    assert L.tmr_split_acc_size(2, 2048, 128, 128) == 2 * 2048 * 128 * 128
+    assert L.tmr_split_acc_size(1, 100, 17, 33) == 128 * 32 * 64
     assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, None, None) == -1
     assert L.tmr_absmax(None, 4, 0, None, None) == -1
 

@@ -202,7 +202,7 @@ def test_split_conv_vs_torch(C, N, H, W, ks, leaky, prec):
     xp = pack_split_x(xd, ks, prec, xmax)
     out = torch.empty((2, N, H, W), device=DEV)
     call("tmr_split_conv_store", ptr(xp), C, None, None, 0, 2, H, W, ks, PREC_CODES[prec], ptr(wp),
-         ptr(wmax), ptr(xmax), ptr(bd), N, int(leaky), ptr(initd), ptr(out), stream())
+         ptr(wmax), ptr(xmax), ptr(bd), N, int(leaky), ptr(initd), ptr(out), 0, stream())
     torch.cuda.synchronize()
     assert normwise(out.cpu().numpy(), ref.numpy()) <= SPLIT_TOL[prec]
 
@@ -236,7 +236,7 @@ def test_split_conv_scales_and_two_sources(scale):
     xp1 = pack_split_x(d["x1"], 3, "fp32", xmax)
     part = torch.empty(tmr_amd._lib.load().tmr_heads_partials_size(N, U, H, W), device=DEV)
     call("tmr_split_conv_heads", ptr(xp0), C0, ptr(uid), ptr(xp1), C1, U, H, W, 3, 0, ptr(wp),
-         ptr(wmax), ptr(xmax), ptr(d["b"]), N, 1, ptr(d["hw"]), None, ptr(part), stream())
+         ptr(wmax), ptr(xmax), ptr(d["b"]), N, 1, ptr(d["hw"]), None, ptr(part), 0, stream())
     o = torch.empty((U, 1, H, W), device=DEV)
     bb = torch.empty((U, 4, H, W), device=DEV)
     hb = torch.zeros(5, device=DEV)
