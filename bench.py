@@ -194,7 +194,7 @@ def main():
             terms = SPLIT_TERMS[prec]
             peak = F16_PEAK_TFLOPS
             kernel_name = ("tmr_split_conv_heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
-                           "+ LeakyReLU + 1x1 heads, v_mfma_f32_32x32x16_%s)"
+                           "+ LeakyReLU + 1x1 heads, v_mfma_f32_16x16x32_%s)"
                            % ("bf16" if prec == "bf16" else "f16"))
             flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
                            "(%s; the fp half runs once per image in tmr_split_conv_store and is "

@@ -154,7 +154,7 @@ int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, co
 
 /* ---- (a11) split-precision 16-bit-MFMA variant of the decoder conv ---------
  * Direct implicit-GEMM kxk conv (ks 1/3/5/7, pad ks/2) on
- * v_mfma_f32_32x32x16_{f16,bf16}; same semantics as tmr_conv_store /
+ * v_mfma_f32_16x16x32_{f16,bf16}; same semantics as tmr_conv_store /
  * tmr_conv_heads (regression_head.py:7-8, matching_net.py:63-75) except that
  * operands are pre-packed 16-bit records:
  *   TMR_PREC_F16X3: x*s = xh + xl, w*s' = wh + wl (fp16, power-of-two scales
@@ -165,9 +165,10 @@ int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, co
  *   TMR_PREC_F16:   one scaled fp16 term.
  * tmr_absmax: *out = max(|x|) (or max(*out, |x|) when accumulate), the scale
  * source for the packs and the conv (F16X3 / F16; NULL allowed for BF16).
- * tmr_split_xpack: x [S][C][H][W] fp32 -> [S][ceil(C/16)][Hp][Wp][rec], zero
- * padded to whole 16x32 tiles plus the ks halo (sizes in BYTES).
- * tmr_split_wpack: w [N][C0+C1][ks][ks] -> [ks*ks][ceil(C0/16)+ceil(C1/16)]
+ * tmr_split_xpack: x [S][C][H][W] fp32 -> [S][ceil(C/32)*halves][Hp][Wp][64 B]
+ * (halves 2 for F16X3: hi, lo), zero padded to whole 16x32 tiles plus the ks
+ * halo (sizes in BYTES).
+ * tmr_split_wpack: w [N][C0+C1][ks][ks] -> [ks*ks][ceil(C0/32)+ceil(C1/32)]
  * [ceil(N/128)*128][rec]; the conv's src0 (per image, C0 channels, packed by
  * xpack with S = images) and src1 (per unit, C1) may both be present.
  * Records: one 64-B record per pixel per 32-channel chunk (F16X3: a hi and a

@@ -216,18 +216,17 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int NC = a.NC0 + a.NC1;
     const int NHC = NC * HALVES;
 
-    // Per-lane halo DMA sources (half-chunk invariant): LDS piece e of the
-    // halo image is plane e / NPIX, record e % NPIX; pad records re-read a
-    // legal address.
-    int hoff[MPW];
-#pragma unroll
-    for (int m = 0; m < MPW; ++m) {
+    // Per-lane halo DMA source of wave-instruction m (half-chunk invariant):
+    // LDS piece e of the halo image is plane e / NPIX, record e % NPIX; pad
+    // records re-read a legal address.  Recomputed per DMA (a few VALU)
+    // rather than held in registers through the main loop.
+    auto hoff = [&](int m) -> int {
         const int e = (wave + NWAVES * m) * 64 + lane;
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
-        hoff[m] = ((ty0 + hy) * a.Wp + (tx0 + hx)) * XREC + q * 16;
-    }
+        return ((ty0 + hy) * a.Wp + (tx0 + hx)) * XREC + q * 16;
+    };
     // Buffer descriptors (SGPRs) over this block's source slabs and weights:
     // every DMA is base + uniform soffset + a 32-bit per-lane voffset, so the
     // loop holds no 64-bit per-lane addresses (and the range check turns any
@@ -248,7 +247,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         for (int m = 0; m < MPW; ++m) {
             const int i = wave + NWAVES * m;
             if (m >= m0 && m < m1 && i < NIH) {
-                buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + i * 1024), hoff[m], soff);
+                buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + i * 1024), hoff(m), soff);
                 ++n;
             }
         }
@@ -349,46 +348,57 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 const int nh = (hc + 1 < NHC && sg * Q < MPW) ? halo_dma(hc + 1, sg * Q, sg * Q + Q) : 0;
                 const int nw = g + D < S ? w_dma(g + D) : 0;
                 const char *wl = Ws + (g % NWB) * WB;
+                // Register pipeline: the A (weight) fragments of a tap are
+                // read during the previous tap of the step, the B (halo)
+                // fragments DB pixel tiles ahead, so an MFMA group never
+                // waits on LDS except at the step's first tap.  F16X3 hi
+                // half-chunks run wh.xh and wl.xh off one B read (NA = 8
+                // A fragments), the others one term (NA = 4).
+                constexpr int NA = (HALVES == 2 && !lo) ? 8 : 4;
+                constexpr int DB = NA == 8 ? 1 : 2;
+                constexpr int NB = DB + 1;
+                const int ntap = min(TPS, T - sg * TPS);
+                auto afrag = [&](int tl, int i) -> V {
+                    return *reinterpret_cast<const V *>(wl + tl * WB1 + (i >> 2) * 4 * WPL + aoff +
+                                                        (i & 3) * 256);
+                };
+                auto bfrag = [&](int tap, int jp) -> V {
+                    const int ky = tap / KS, kx = tap % KS;
+                    return *reinterpret_cast<const V *>(
+                        hl + boff + (((jp >> 1) + ky) * HC + kx + (jp & 1) * 16) * 16);
+                };
+                V aw[2][NA];
+                V bx[NB];
+#pragma unroll
+                for (int i = 0; i < NA; ++i) aw[0][i] = afrag(0, i);
+#pragma unroll
+                for (int d = 0; d < DB; ++d) bx[d] = bfrag(sg * TPS, d);
+                __builtin_amdgcn_sched_group_barrier(0x100, NA + DB, 0);
 #pragma unroll
                 for (int tl = 0; tl < TPS; ++tl) {
+                    if (tl >= ntap) break;
                     const int tap = sg * TPS + tl;
-                    if (tap >= T) break;
-                    const int ky = tap / KS, kx = tap % KS;
-                    // passes over the pixel tiles: F16X3 hi = wh.xh then wl.xh
-                    // (the xh fragments are read twice: 4 live A fragments
-                    // instead of 8 keep the loop free of spills), lo = wh.xl,
-                    // one-term = w.x.  A 16x16x32 MFMA per (n tile, pixel tile).
-                    constexpr int NPASS = (HALVES == 2 && !lo) ? 2 : 1;
+                    const bool more = tl + 1 < ntap;
 #pragma unroll
-                    for (int pass = 0; pass < NPASS; ++pass) {
-                        V aw[4];
+                    for (int jp = 0; jp < 8; ++jp) {
+                        const int q = tl * 8 + jp, qn = q + DB;
+                        const bool rb = jp + DB < 8 || more;
+                        if (rb) bx[qn % NB] = jp + DB < 8 ? bfrag(tap, jp + DB) : bfrag(tap + 1, jp + DB - 8);
+                        // next tap's A: one fragment per pixel tile (hi), the
+                        // first four tiles (one-term)
+                        const bool ra = more && jp < NA;
+                        if (ra) aw[(tl + 1) & 1][jp] = afrag(tl + 1, jp);
+                        const V b = bx[q % NB];
 #pragma unroll
-                        for (int in = 0; in < 4; ++in)
-                            aw[in] = *reinterpret_cast<const V *>(wl + tl * WB1 + pass * 4 * WPL + aoff +
-                                                                  in * 16 * 16);
-#pragma unroll
-                        for (int jp = 0; jp < 8; ++jp) {
-                            const V bx = *reinterpret_cast<const V *>(
-                                hl + boff + (((jp >> 1) + ky) * HC + kx + (jp & 1) * 16) * 16);
-#pragma unroll
-                            for (int in = 0; in < 4; ++in) acc[in][jp] = mma(aw[in], bx, acc[in][jp]);
-                        }
-                        // pin the interleave: the A fragments and B(0) first,
-                        // then per pixel tile its 4 MFMAs with B(jp+1) read in
-                        // their shadow.  Unconstrained, hipcc hoists later
-                        // fragments and spills inside the loop, and the
-                        // reloads (vmcnt(0)) drain the counted DMA pipeline.
-                        __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
-#pragma unroll
-                        for (int jp = 0; jp < 7; ++jp) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                        for (int i = 0; i < NA; ++i) acc[i & 3][jp] = mma(aw[tl & 1][i], b, acc[i & 3][jp]);
+                        if (rb && ra)
+                            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        else if (rb || ra)
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                        }
-                        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-                        __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     }
                 }
+                __builtin_amdgcn_sched_barrier(0);
                 // the next step needs W(g+1) and, after a half-chunk's last
                 // step, the whole halo of hc+1: leave only younger DMAs in
                 // flight (in-order completion; halo issued before weights)
