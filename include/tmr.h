@@ -246,6 +246,18 @@ int tmr_nms(const float *logits, const float *box, const float *ref, const int32
             float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
             int32_t *kept, void *work, void *stream);
 
+/* ---- (§8f f1) streaming mapper statistics ---------------------------------
+ * Per image b of x [B][n] fp32 (the backbone feature the mapper computes,
+ * mapper.py:94), out[b] = {mean, std, max, sparsity} (fp64), as
+ * mapper.py:97-101 computes them with numpy: mean = np.mean(f) and
+ * std = np.std(f) (population) each correctly rounded to fp32 from an fp64
+ * evaluation (numpy's float32 pairwise sums differ by a few fp32 ulps),
+ * max = np.max(f) exactly, sparsity = np.mean(f <= 0) = count / n exactly.
+ * Deterministic (fixed reduction order).  `work` holds
+ * tmr_feature_stats_work_size(B) bytes. */
+int64_t tmr_feature_stats_work_size(int B);
+int tmr_feature_stats(const float *x, int B, int64_t n, void *work, double *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

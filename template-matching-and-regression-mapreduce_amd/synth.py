@@ -101,3 +101,21 @@ def reference_state_dict(seed: int, cin: int = 256, emb: int = 512, num_layers: 
     P["ltrbs_head.head.0.weight"] = torch.randn(4, d, 1, 1, generator=g) * 0.01
     P["ltrbs_head.head.0.bias"] = torch.zeros(4)
     return {k_: v.float().to(device) for k_, v in P.items()}
+
+
+def sam_features_device(seeds, C: int = 256, H: int = 64, W: int = 64, device="cuda"):
+    """Device-side counterpart of sam_features for the streaming driver: per
+    seed a standard normal [C,H,W] from a seeded torch generator on `device`,
+    LayerNorm over C (eps 1e-6).  Not bit-identical to sam_features (a
+    different PRNG); used where the features are only workload, not a
+    parity input."""
+    import torch
+
+    out = torch.empty((len(seeds), C, H, W), device=device, dtype=torch.float32)
+    g = torch.Generator(device=device)
+    for i, s in enumerate(seeds):
+        g.manual_seed(int(s))
+        out[i].normal_(generator=g)
+    mu = out.mean(dim=1, keepdim=True)
+    var = (out - mu).pow(2).mean(dim=1, keepdim=True)
+    return (out - mu) / torch.sqrt(var + 1e-6)
