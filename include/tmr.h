@@ -201,6 +201,8 @@ int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, con
  * in that layout (indexed by unit_image), e.g. the per-image fp half. */
 #define TMR_SPLIT_TILED_OUT 1
 #define TMR_SPLIT_TILED_INIT 2
+#define TMR_SPLIT_INIT_BCAST 4  /* acc_init is ONE slab shared by every unit
+                                 * (e.g. the folded projection bias plane) */
 int64_t tmr_split_acc_size(int U, int N, int H, int W);
 int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
                          int C1, int U, int H, int W, int ks, int prec, const void *wpack,

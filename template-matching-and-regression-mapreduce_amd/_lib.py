@@ -41,7 +41,7 @@ TEMPLATE_PROTOTYPE = 1
 
 # decoder-conv precision modes of the split 16-bit-MFMA kernel (include/tmr.h)
 PREC_CODES = {"fp32": 0, "bf16": 1, "f16": 2}
-SPLIT_TILED_OUT, SPLIT_TILED_INIT = 1, 2
+SPLIT_TILED_OUT, SPLIT_TILED_INIT, SPLIT_INIT_BCAST = 1, 2, 4
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

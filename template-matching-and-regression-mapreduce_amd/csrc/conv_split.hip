@@ -56,8 +56,17 @@ typedef __attribute__((address_space(3))) void *lds_ptr_t;
 constexpr int BM = 128;      // output channels per block
 constexpr int TH = 16;       // output rows per block
 constexpr int TW = 32;       // output cols per block
-constexpr int NTHREADS = 512;
-constexpr int NWAVES = 8;
+// waves per block: 8 (2 along n x 4 along rows, 128 accumulator VGPRs, two
+// waves per SIMD) or 4 (1 x 4, 256 accumulators, one wave per SIMD: half
+// the LDS fragment reads per MFMA)
+#ifndef TMR_SPLIT_NW
+#define TMR_SPLIT_NW 8
+#endif
+constexpr int NWAVES = TMR_SPLIT_NW;
+constexpr int NTHREADS = NWAVES * 64;
+constexpr int WNS = NWAVES == 8 ? 2 : 1;  // waves along n
+constexpr int NIN = 8 / WNS;              // 16-channel n fragments per wave
+constexpr int ACCW = NIN * 8 * 64 * 4;    // accumulator floats per wave
 constexpr int NHEAD = 5;
 constexpr int CCH = 32;      // channels per chunk (one MFMA K)
 constexpr int P = 4;         // 16-B pieces per activation record
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     const int l16 = lane & 15, kg = lane >> 4;
-    const int wn = wave & 1, wpix = wave >> 1;
+    const int wn = wave % WNS, wpix = wave / WNS;
 
     // XCD-aware bijective remap (the 8 XCDs take blocks round robin): the NT
     // channel tiles of a pixel tile run back to back on one XCD and share its
@@ -221,7 +230,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // records re-read a legal address.  Recomputed per DMA (a few VALU)
     // rather than held in registers through the main loop.
     auto hoff = [&](int m) -> int {
-        const int e = (wave + NWAVES * m) * 64 + lane;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));  // opaque: keeps LICM from hoisting (and spilling) the offsets
+        const int e = (wave + NWAVES * m) * 64 + ln;
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
@@ -288,25 +299,26 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // 16x16 accumulator: column = pixel l16, row = n 4*kg + r.
     const float sxw = PR::SCALED ? split_scale(a.xmax) * split_scale(a.wmax) : 1.0f;
     const int HW = a.H * a.W;
-    f32x4 acc[4][8];
+    f32x4 acc[NIN][8];
     // tiled acc layout: [slab][nt][mt][wave][in*8+jp][lane][4] fp32, i.e. each
     // accumulator register set is one contiguous KB per wave (no masking)
-    const size_t tile_off = ((((size_t)img * a.NT + nt) * a.MT + mt) * NWAVES + wave) * (32 * 64 * 4);
+    const int islab = (a.flags & TMR_SPLIT_INIT_BCAST) ? 0 : img;  // acc_init slab
+    const size_t tile_off = ((((size_t)islab * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW;
     if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT)) {
         const f32x4 *ai = reinterpret_cast<const f32x4 *>(a.acc_init + tile_off) + lane;
 #pragma unroll
-        for (int in = 0; in < 4; ++in)
+        for (int in = 0; in < NIN; ++in)
 #pragma unroll
             for (int jp = 0; jp < 8; ++jp) acc[in][jp] = ai[(in * 8 + jp) * 64] * sxw;
     } else if (a.acc_init) {
-        const float *ai = a.acc_init + (size_t)img * a.N * HW;
+        const float *ai = a.acc_init + (size_t)islab * a.N * HW;
 #pragma unroll
         for (int jp = 0; jp < 8; ++jp) {
             const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
             const bool pin = y < a.H && x < a.W;
             const int pix = min(y, a.H - 1) * a.W + min(x, a.W - 1);
 #pragma unroll
-            for (int in = 0; in < 4; ++in)
+            for (int in = 0; in < NIN; ++in)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int n = nt * BM + wn * 64 + in * 16 + 4 * kg + r;
@@ -316,7 +328,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         }
     } else {
 #pragma unroll
-        for (int in = 0; in < 4; ++in)
+        for (int in = 0; in < NIN; ++in)
 #pragma unroll
             for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
@@ -354,13 +366,14 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 // waits on LDS except at the step's first tap.  F16X3 hi
                 // half-chunks run wh.xh and wl.xh off one B read (NA = 8
                 // A fragments), the others one term (NA = 4).
-                constexpr int NA = (HALVES == 2 && !lo) ? 8 : 4;
-                constexpr int DB = NA == 8 ? 1 : 2;
+                constexpr int NA = (HALVES == 2 && !lo) ? 2 * NIN : NIN;
+                constexpr int DB = NA >= 8 ? 1 : 2;
+                constexpr int APG = NA >= 8 ? NA / 8 : 1;  // next-tap A reads per pixel tile
                 constexpr int NB = DB + 1;
                 const int ntap = min(TPS, T - sg * TPS);
-                auto afrag = [&](int tl, int i) -> V {
-                    return *reinterpret_cast<const V *>(wl + tl * WB1 + (i >> 2) * 4 * WPL + aoff +
-                                                        (i & 3) * 256);
+                auto afrag = [&](int tl, int i) -> V {  // term i / NIN, n fragment i % NIN
+                    return *reinterpret_cast<const V *>(wl + tl * WB1 + (i / NIN) * 4 * WPL + aoff +
+                                                        (i % NIN) * 256);
                 };
                 auto bfrag = [&](int tap, int jp) -> V {
                     const int ky = tap / KS, kx = tap % KS;
@@ -386,14 +399,20 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                         if (rb) bx[qn % NB] = jp + DB < 8 ? bfrag(tap, jp + DB) : bfrag(tap + 1, jp + DB - 8);
                         // next tap's A: one fragment per pixel tile (hi), the
                         // first four tiles (one-term)
-                        const bool ra = more && jp < NA;
-                        if (ra) aw[(tl + 1) & 1][jp] = afrag(tl + 1, jp);
+                        const int na = (more && jp * APG < NA) ? APG : 0;
+#pragma unroll
+                        for (int j = 0; j < APG; ++j)
+                            if (j < na) aw[(tl + 1) & 1][jp * APG + j] = afrag(tl + 1, jp * APG + j);
                         const V b = bx[q % NB];
 #pragma unroll
-                        for (int i = 0; i < NA; ++i) acc[i & 3][jp] = mma(aw[tl & 1][i], b, acc[i & 3][jp]);
-                        if (rb && ra)
+                        for (int i = 0; i < NA; ++i)
+                            acc[i % NIN][jp] = mma(aw[tl & 1][i], b, acc[i % NIN][jp]);
+                        const int nr = (rb ? 1 : 0) + na;
+                        if (nr == 3)
+                            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                        else if (nr == 2)
                             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                        else if (rb || ra)
+                        else if (nr == 1)
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     }
@@ -419,10 +438,10 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         // raw conv result (scaled back) in the tiled acc layout of slab u: the
         // acc_init of a later launch; bias / activation are not applied here
         f32x4 *o = reinterpret_cast<f32x4 *>(
-                       a.out + ((((size_t)u * a.NT + nt) * a.MT + mt) * NWAVES + wave) * (32 * 64 * 4)) +
+                       a.out + ((((size_t)u * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW) +
                    lane;
 #pragma unroll
-        for (int in = 0; in < 4; ++in)
+        for (int in = 0; in < NIN; ++in)
 #pragma unroll
             for (int jp = 0; jp < 8; ++jp) o[(in * 8 + jp) * 64] = acc[in][jp] * inv;
         return;
@@ -445,7 +464,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
         for (int k = 0; k < NHEAD; ++k) hs[jp][k] = 0.0f;
 #pragma unroll
-    for (int in = 0; in < 4; ++in)
+    for (int in = 0; in < NIN; ++in)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int nl = wn * 64 + in * 16 + 4 * kg + r;
@@ -480,7 +499,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 hs[jp][k] += __shfl_xor(hs[jp][k], 32);
             }
         __syncthreads();  // sb / shw reads are done before red is written
-        if (wn == 1 && kg == 0) {
+        if (WNS == 2 && wn == 1 && kg == 0) {
 #pragma unroll
             for (int jp = 0; jp < 8; ++jp)
 #pragma unroll
@@ -494,7 +513,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 if (y >= a.H || x >= a.W) continue;
 #pragma unroll
                 for (int k = 0; k < NHEAD; ++k) {
-                    const float v = hs[jp][k] + red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16];
+                    const float v = hs[jp][k] + (WNS == 2 ? red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16] : 0.0f);
                     a.partials[(((size_t)nt * NHEAD + k) * a.U + u) * HW + (size_t)y * a.W + x] = v;
                 }
             }

@@ -27,8 +27,8 @@ import numpy as np
 import torch
 
 from . import host
-from ._lib import (PREC_CODES, SPLIT_TILED_INIT, SPLIT_TILED_OUT, TMRError, call, load, ptr,
-                   require_gpu, stream)
+from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_TILED_INIT, SPLIT_TILED_OUT, TMRError,
+                   call, load, ptr, require_gpu, stream)
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
@@ -172,19 +172,20 @@ def fold_proj(w: torch.Tensor, cp: int, proj_w: torch.Tensor, proj_b: torch.Tens
 
 
 def pack_split_up(f: torch.Tensor, upsample: bool, ks: int, precision: str,
-                  xmax: torch.Tensor) -> torch.Tensor:
-    """SAM features [S,Cin,h,w] -> records of [up2x(f) or f; 1] (tmr_split_xpack_up)."""
+                  xmax: torch.Tensor, ones: bool = True) -> torch.Tensor:
+    """SAM features [S,Cin,h,w] -> records of [up2x(f) or f; 1] (tmr_split_xpack_up;
+    without the constant-1 channel when ones=False)."""
     require_gpu(f, "features")
     f = f.float().contiguous()
     S, Cin, Hin, Win = f.shape
     H, W = (2 * Hin, 2 * Win) if upsample else (Hin, Win)
     pc = prec_code(precision)
-    n = load().tmr_split_xpack_size(S, Cin + 1, H, W, ks, pc)
+    n = load().tmr_split_xpack_size(S, Cin + int(ones), H, W, ks, pc)
     if n <= 0:
         raise TMRError(f"unsupported feature shape {tuple(f.shape)}")
     out = torch.empty(n, device=f.device, dtype=torch.uint8)
-    call("tmr_split_xpack_up", ptr(f), S, Cin, Hin, Win, int(upsample), 1, ks, pc, ptr(xmax),
-         ptr(out), stream())
+    call("tmr_split_xpack_up", ptr(f), S, Cin, Hin, Win, int(upsample), int(ones), ks, pc,
+         ptr(xmax), ptr(out), stream())
     return out
 
 
@@ -314,24 +315,52 @@ class TMREngine:
                 pk = lambda w_, c0: pk0(w_)  # noqa: E731
             split = None
             if fold:
-                # fp half folded through input_proj: [N, Cin+1, k, k]
+                # fp half folded through input_proj: [N, Cin+1, k, k]; the
+                # constant-1 channel's conv is a fixed plane per map size
+                # (_bias_plane), so the GEMM runs on the Cin channels only
                 Wf = fold_proj(W, c0_full, pw_, pb_)
-                cf = Wf.shape[1]
+                cf = Wf.shape[1] - 1
+                wbias = Wf[:, cf:].contiguous()
+                Wf = Wf[:, :cf].contiguous()
                 if split_c0:
                     split = (pk(Wf, cf), pk(W[:, c0_full:].contiguous(), 0),
                              torch.zeros(N, device=W.device, dtype=torch.float32))
                     full = None
                 else:
                     full = pk(torch.cat([Wf, W[:, c0_full:]], 1).contiguous(), cf)
-                return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
+                return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split, wbias
             if split_c0:
                 split = (pk(W[:, :split_c0].contiguous(), split_c0), pk(W[:, split_c0:].contiguous(), 0),
                          torch.zeros(N, device=W.device, dtype=torch.float32))
             full = None if split_c0 else pk(W, c0_full)
-            return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split
+            return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split, None
 
         return self._cache.get(f"fused_dec{split_c0}_{algo}_{cfg.precision}_{int(fold)}", tensors,
                                build)
+
+    def _bias_plane(self, wbias: torch.Tensor, H: int, W: int) -> torch.Tensor:
+        """conv'(1) of the folded projection bias (wbias [N,1,k,k]): the
+        constant-1 input channel of [up2x(f); 1], zero in the conv padding
+        like fp's, as one slab in the split kernel's tiled accumulator
+        layout (acc_init with TMR_SPLIT_INIT_BCAST).  Cached per weights
+        version and map size."""
+        N, _, ks, _ = wbias.shape
+        prec = self.cfg.precision
+
+        def build():
+            dev = wbias.device
+            ones = torch.ones((1, 1, H, W), device=dev, dtype=torch.float32)
+            one = torch.ones(1, device=dev, dtype=torch.float32)
+            xp = pack_split_x(ones, ks, prec, one)
+            wp, wmax = pack_split_w(wbias, 1, prec)
+            plane = torch.empty(load().tmr_split_acc_size(1, N, H, W), device=dev, dtype=torch.float32)
+            zero = torch.zeros(N, device=dev, dtype=torch.float32)
+            call("tmr_split_conv_store", ptr(xp), 1, None, None, 0, 1, H, W, ks, prec_code(prec),
+                 ptr(wp), ptr(wmax), ptr(one), ptr(zero), N, 0, None, ptr(plane), SPLIT_TILED_OUT,
+                 stream())
+            return plane
+
+        return self._cache.get(f"bias_plane_{H}x{W}_{prec}", [wbias], build)
 
     def _conv(self, name: str, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool):
         """One nn.Conv2d (+ LeakyReLU) of the general-depth stack on the
@@ -451,11 +480,14 @@ class TMREngine:
             wino, splitk = algo == "wino", algo == "split"
             ks = cfg.decoder_kernel_size
             fold = splitk and cfg.fusion and self.fold_proj and feats is not None
-            wp, bias, N, Cw, hw, hb, split = self._fused_decoders(C0 if share else 0, algo, fold)
+            wp, bias, N, Cw, hw, hb, split, wbias = self._fused_decoders(C0 if share else 0, algo,
+                                                                          fold)
             if Cw != C0 + C1:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
-            if fold:  # the fp half runs on [up2x(f); 1] with Cin+1 channels
-                C0 = feats.shape[1] + 1
+            bplane = None
+            if fold:  # the fp half runs on up2x(f) (Cin channels) + the bias plane
+                C0 = feats.shape[1]
+                bplane = self._bias_plane(wbias, H, W)
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
             acc0 = None
@@ -470,7 +502,7 @@ class TMREngine:
                     xmax1 = tm_max
                 else:
                     xmax1 = absmax(tm_max, xmax0.clone())
-                xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0)
+                xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0, ones=False)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
             elif splitk:
@@ -490,9 +522,12 @@ class TMREngine:
                 if splitk:  # acc0 in the kernel's tiled accumulator layout (private)
                     acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
                                        dtype=torch.float32)
+                    fl = SPLIT_TILED_OUT
+                    if bplane is not None:
+                        fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST
                     call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
-                         ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0, None,
-                         ptr(acc0), SPLIT_TILED_OUT, stream())
+                         ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0,
+                         ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
                 else:
                     acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
                 if splitk:
@@ -510,10 +545,13 @@ class TMREngine:
                 ev[0].record()
             s0 = ptr(src0) if src0 is not None else None
             a0 = ptr(acc0) if acc0 is not None else None
+            fl = SPLIT_TILED_INIT if a0 is not None else 0
+            if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
+                a0, fl = ptr(bplane), SPLIT_TILED_INIT | SPLIT_INIT_BCAST
             if splitk:
                 call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                      U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
-                     a0, ptr(part), SPLIT_TILED_INIT if a0 is not None else 0, stream())
+                     a0, ptr(part), fl, stream())
             elif wino:
                 call("tmr_wino_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
                      ptr(bias), N, 1, ptr(hw), a0, ptr(part), stream())
