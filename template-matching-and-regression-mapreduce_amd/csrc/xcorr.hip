@@ -99,7 +99,7 @@ __device__ void corr_dispatch(int w, const float *xs, int W, int x0, int r0, con
 // loads (s_load_dwordx16 rows) for the wave-uniform taps.
 __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restrict__ tmpl,
                                                   float *__restrict__ outp) {
-    extern __shared__ float xs[];
+    extern __shared__ __attribute__((aligned(16))) float xs[];
     const int band = blockIdx.x, c = blockIdx.y, img = blockIdx.z;
     const int H = a.H, W = a.W;
     // wave-uniform unit range and descriptors (SGPRs): the template taps then
@@ -114,7 +114,12 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
     const int rlo = max(yb0 - hmax / 2, 0), rhi = min(yb1 + hmax / 2, H);
     const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
     const int nld = (rhi - rlo) * W;
-    for (int e = threadIdx.x; e < nld; e += NT) xs[e] = fc[(size_t)rlo * W + e];
+    if ((W & 3) == 0) {  // 16-B staging loads (rows are 16-B aligned)
+        const float4 *src4 = reinterpret_cast<const float4 *>(fc + (size_t)rlo * W);
+        float4 *dst4 = reinterpret_cast<float4 *>(xs);
+        for (int e = threadIdx.x; e < nld / 4; e += NT) dst4[e] = src4[e];
+    } else
+        for (int e = threadIdx.x; e < nld; e += NT) xs[e] = fc[(size_t)rlo * W + e];
     // zero the slack rows/cols the 4x4 register blocks may over-read
     for (int e = nld + threadIdx.x; e < a.LR * W + XSLACK; e += NT) xs[e] = 0.0f;
     __syncthreads();
@@ -145,11 +150,15 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
             }
         }
         const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
-        const int nbx = (Wo + RX - 1) / RX, nby = (nv + RY - 1) / RY;
+        // x blocks per row group padded to a multiple of 16: a 16-lane group of
+        // a ds_read_b128 never straddles two row groups (bank conflicts)
+        const int nbx = ((Wo + RX - 1) / RX + 15) / 16 * 16, nby = (nv + RY - 1) / RY;
+        const int nbx_v = (Wo + RX - 1) / RX;
         // LDS row of conv row (ya - ph): ya - ph - rlo
         const int rbase = ya - ph - rlo;
         for (int task = threadIdx.x; task < nbx * nby; task += NT) {
             const int x0 = (task % nbx) * RX, r0 = (task / nbx) * RY;
+            if (task % nbx >= nbx_v) continue;
             float acc[RY][RX];
 #pragma unroll
             for (int r = 0; r < RY; ++r)
