@@ -175,7 +175,10 @@ struct Geo {
     static constexpr int NPIX = (HR * HC + 15) / 16 * 16;     // halo records per plane
     static constexpr int HPL = NPIX * 16;                      // halo plane bytes (256-B multiple)
     static constexpr int NIH = (P * HPL + 1023) / 1024;        // halo DMA wave-instructions
-    static constexpr int HB = NIH * 1024;                      // bytes per halo buffer
+    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;    // halo DMAs per wave per half-chunk
+    // bytes per halo buffer, padded to MPW instructions for every wave (the
+    // pad KB receives re-read records and is never read)
+    static constexpr int HB = MPW * NWAVES * 1024;
     static constexpr int NPLW = Prec<PREC>::WREC / 16;         // weight planes per tap (8 or 4)
     static constexpr int WB1 = NPLW * WPL;                     // weight bytes per tap
     static constexpr bool fits(int tps, int nwb) { return 2 * HB + nwb * tps * WB1 <= 160 * 1024; }
@@ -184,10 +187,40 @@ struct Geo {
     static constexpr int NWB = fits(TPS, 3) ? 3 : 2;
     static constexpr int SPC = (T + TPS - 1) / TPS;            // steps per half-chunk
     static constexpr int WB = TPS * WB1;                       // bytes per weight buffer
-    static constexpr int WPW = (TPS * NPLW * 2 + NWAVES - 1) / NWAVES;  // weight DMAs per wave per step
-    static constexpr int MPW = (NIH + NWAVES - 1) / NWAVES;    // halo DMAs per wave per half-chunk
-    static constexpr int Q = (MPW + SPC - 1) / SPC;            // ... issued per step
+    static constexpr int Q = (MPW + SPC - 1) / SPC;            // halo DMAs per wave issued per step
     static constexpr size_t LDS = 2 * (size_t)HB + NWB * (size_t)WB;
+    // per-wave DMA counts of step sg of a half-chunk of kind `part` (the
+    // kernel issues, in this order, the step's share of the next halo, then
+    // the weights of step g + NWB - 1)
+    static constexpr int ipt(bool lo) { return lo ? 8 : NPLW * 2; }
+    static constexpr int nh(int sg) { return MPW - sg * Q < Q ? (MPW - sg * Q > 0 ? MPW - sg * Q : 0) : Q; }
+    static constexpr bool lo_of(int sgx, int part, int halves) { return halves == 2 && ((sgx / SPC + part) & 1); }
+    static constexpr int nw(int sg, int part, int halves) {
+        return (T - ((sg + NWB - 1) % SPC) * TPS < TPS ? T - ((sg + NWB - 1) % SPC) * TPS : TPS) *
+               ipt(lo_of(sg + NWB - 1, part, halves)) / NWAVES;
+    }
+    // DMAs allowed in flight at the end of step sg: those issued after the
+    // weights of step g+1 (issued NWB-2 steps earlier), and at a half-chunk's
+    // last step none of the next halo (steps of the previous half-chunk are
+    // counted with the other part; before the first steps the prologue has
+    // already completed everything they need)
+    static constexpr int allowed(int sg, int part, int halves) {
+        int n = 0;
+        for (int j = 0; j <= NWB - 3; ++j) {
+            int s = sg - j, p = part;
+            if (s < 0) { s += SPC; p = halves == 2 ? part ^ 1 : part; }
+            n += nh(s) + nw(s, p, halves);
+        }
+        if (sg == SPC - 1) {
+            int last = 0;  // last step of this half-chunk that issues halo DMAs
+            for (int s = 0; s < SPC; ++s)
+                if (nh(s) > 0) last = s;
+            int after = 0;
+            for (int s = last; s < SPC; ++s) after += nw(s, part, halves);
+            n = n < after ? n : after;
+        }
+        return n;
+    }
     static_assert(fits(TPS, NWB), "LDS");
 };
 
@@ -196,8 +229,8 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     typedef Prec<PREC> PR;
     typedef typename PR::V V;
     typedef Geo<KS, PREC> G;
-    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q, NIH = G::NIH;
-    constexpr int HB = G::HB, WB = G::WB, WB1 = G::WB1, NWB = G::NWB, WPW = G::WPW;
+    constexpr int HC = G::HC, T = G::T, MPW = G::MPW, Q = G::Q;
+    constexpr int HB = G::HB, WB = G::WB, WB1 = G::WB1, NWB = G::NWB;
     constexpr int TPS = G::TPS, SPC = G::SPC, HPL = G::HPL, NPIX = G::NPIX;
     constexpr int HALVES = PR::HALVES, WREC = PR::WREC;
     constexpr int D = NWB - 1;  // weight DMA lookahead (steps)
@@ -223,7 +256,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int ty0 = (mt / a.TXN) * TH, tx0 = (mt % a.TXN) * TW;
     const int img = a.unit_image ? a.unit_image[u] : u;
     const int NC = a.NC0 + a.NC1;
-    const int NHC = NC * HALVES;
+
 
     // Per-lane halo DMA source of wave-instruction m (half-chunk invariant):
     // LDS piece e of the halo image is plane e / NPIX, record e % NPIX; pad
@@ -248,21 +281,14 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         (void *)(h0 ? a.x0 + (size_t)img * h0 * cstride : a.x1), (short)0, h0 * cstride, 0x00020000);
     const __amdgpu_buffer_rsrc_t xr1 = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(h1 ? a.x1 + (size_t)u * h1 * cstride : a.x0), (short)0, h1 * cstride, 0x00020000);
-    // issue this wave's halo instructions m0 <= m < m1 of half-chunk hc; returns the count
-    auto halo_dma = [&](int hc, int m0, int m1) -> int {
+    // this wave's halo instruction m of half-chunk hc (every wave issues
+    // MPW per half-chunk; hc == NHC, past the end, reads zeros via the
+    // descriptor range check into the free buffer)
+    auto halo_dma1 = [&](int hc, int m) {
         const bool s0 = hc < h0;
         const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;
         char *dst = Hs + (hc & 1) * HB;
-        int n = 0;
-#pragma unroll
-        for (int m = 0; m < MPW; ++m) {
-            const int i = wave + NWAVES * m;
-            if (m >= m0 && m < m1 && i < NIH) {
-                buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + i * 1024), hoff(m), soff);
-                ++n;
-            }
-        }
-        return n;
+        buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + (wave + NWAVES * m) * 1024), hoff(m), soff);
     };
     // weights of flat step g: half-chunk g / SPC (hi: wh and wl planes, lo:
     // wh only), taps TPS*(g % SPC)...; instruction i of the step = tap i/IPT,
@@ -271,26 +297,19 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(a.wp + (size_t)nt * BM * WREC), (short)0, T * tapstride - nt * BM * WREC, 0x00020000);
     const int wlane = lane * WREC;
-    auto w_dma = [&](int g) -> int {
+    // this wave's weight instruction m of flat step g, whose shape (lo, taps)
+    // the caller knows at compile time: ipt instructions per tap, every wave
+    // issuing the same count (ipt is a multiple of NWAVES).  g == S (past the
+    // end) loads harmless in-range bytes into the free buffer.
+    auto w_dma1 = [&](int g, int ipt, int m) {
         const int hc = g / SPC, t0 = (g - hc * SPC) * TPS;
         const int c = hc / HALVES;
-        const bool lo = HALVES == 2 && (hc & 1);
-        const int ipt = lo ? 8 : G::NPLW * 2;  // instructions per tap
-        const int ni = min(TPS, T - t0) * ipt;
         const uint32_t src = (uint32_t)t0 * tapstride + (uint32_t)c * a.Npad * WREC;
         char *dst = Ws + (g % NWB) * WB;
-        int n = 0;
-#pragma unroll
-        for (int m = 0; m < WPW; ++m) {
-            const int i = wave + NWAVES * m;
-            if (i < ni) {
-                const int tl = i / ipt, wi = i - tl * ipt;
-                const uint32_t so = src + (uint32_t)tl * tapstride + ((wi & 1) * 64 * WREC + (wi >> 1) * 16);
-                buffer_lds16(wr, (lds_ptr_t)(dst + tl * WB1 + wi * 1024), wlane, so);
-                ++n;
-            }
-        }
-        return n;
+        const int i = wave + NWAVES * m;
+        const int tl = i / ipt, wi = i - tl * ipt;
+        const uint32_t so = src + (uint32_t)tl * tapstride + ((wi & 1) * 64 * WREC + (wi >> 1) * 16);
+        buffer_lds16(wr, (lds_ptr_t)(dst + tl * WB1 + wi * 1024), wlane, so);
     };
 
     // accumulators start at acc_init (scaled into the accumulator's units by
@@ -340,9 +359,18 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int aoff = kg * WPL + (wn * 64 + l16) * 16;
     const int boff = kg * HPL + (wpix * 4 * HC + l16) * 16;
 
-    const int S = NHC * SPC;  // barrier steps
-    halo_dma(0, 0, MPW);
-    for (int g0 = 0; g0 < D && g0 < S; ++g0) w_dma(g0);
+    // compile-time shape of step sg of a half-chunk of kind lo
+    auto ipt_of = [](bool lo_) { return lo_ ? 8 : G::NPLW * 2; };  // weight DMAs per tap
+#pragma unroll
+    for (int m = 0; m < MPW; ++m) halo_dma1(0, m);
+    // prologue weights: steps 0..D-1 of half-chunk 0 (a hi one)
+#pragma unroll
+    for (int g0 = 0; g0 < D; ++g0) {
+        const bool lo0 = HALVES == 2 && ((g0 / SPC) & 1);
+        const int nt0 = min(TPS, T - (g0 % SPC) * TPS) * ipt_of(lo0) / NWAVES;
+#pragma unroll
+        for (int m = 0; m < nt0; ++m) w_dma1(g0, ipt_of(lo0), m);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
@@ -352,13 +380,26 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
             constexpr bool lo = part == 1;  // F16X3 lo half-chunk: wh . xl only
             const int hc = c * HALVES + part;
             const char *hl = Hs + (hc & 1) * HB;
-#pragma unroll
-            for (int sg = 0; sg < SPC; ++sg) {
+            // the half-chunk's steps as compile-time indices (DMA counts and
+            // waits are constants): step(integral_constant<int, sg>)
+            auto step = [&](auto sg_c) {
+                constexpr int sg = decltype(sg_c)::value;
                 const int g = hc * SPC + sg;
-                // DMAs for later steps: halo of half-chunk hc+1 (buffer last
-                // read in hc-1), then the weights of step g+D (last read in g-1)
-                const int nh = (hc + 1 < NHC && sg * Q < MPW) ? halo_dma(hc + 1, sg * Q, sg * Q + Q) : 0;
-                const int nw = g + D < S ? w_dma(g + D) : 0;
+                // DMAs for later steps, issued one per pixel-tile MFMA group
+                // from the step's second group on (not in the post-barrier
+                // bubble): first this step's share of the halo of half-chunk
+                // hc+1 (buffer last read in hc-1), then the weights of step
+                // g+D (buffer last read in g-1).  Counts are compile-time and
+                // the same in every wave.
+                constexpr int nh = G::nh(sg);
+                constexpr bool loD = G::lo_of(sg + D, part, HALVES);
+                constexpr int nw = G::nw(sg, part, HALVES);
+                auto dma_slot = [&](int k) {  // DMA k of this step (k < nh + nw)
+                    if (k < nh)
+                        halo_dma1(hc + 1, sg * Q + k);
+                    else
+                        w_dma1(g + D, ipt_of(loD), k - nh);
+                };
                 const char *wl = Ws + (g % NWB) * WB;
                 // Register pipeline: the A (weight) fragments of a tap are
                 // read during the previous tap of the step, the B (halo)
@@ -370,7 +411,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 constexpr int DB = NA >= 8 ? 1 : 2;
                 constexpr int APG = NA >= 8 ? NA / 8 : 1;  // next-tap A reads per pixel tile
                 constexpr int NB = DB + 1;
-                const int ntap = min(TPS, T - sg * TPS);
+                constexpr int ntap = T - sg * TPS < TPS ? T - sg * TPS : TPS;
                 auto afrag = [&](int tl, int i) -> V {  // term i / NIN, n fragment i % NIN
                     return *reinterpret_cast<const V *>(wl + tl * WB1 + (i / NIN) * 4 * WPL + aoff +
                                                         (i % NIN) * 256);
@@ -403,6 +444,10 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
                         for (int j = 0; j < APG; ++j)
                             if (j < na) aw[(tl + 1) & 1][jp * APG + j] = afrag(tl + 1, jp * APG + j);
+                        // DMA slot k = q - 1 (groups 1.. of the step)
+                        const int k = q - 1;
+                        const bool dm = k >= 0 && k < nh + nw;
+                        if (dm) dma_slot(k);
                         const V b = bx[q % NB];
 #pragma unroll
                         for (int i = 0; i < NA; ++i)
@@ -414,9 +459,15 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                         else if (nr == 1)
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        if (dm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     }
                 }
+                // slots beyond the step's groups (not reached by the shapes
+                // built here, kept for safety)
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (k >= ntap * 8 - 1 && k < nh + nw) dma_slot(k);
                 __builtin_amdgcn_sched_barrier(0);
                 // the next step needs W(g+1) and, after a half-chunk's last
                 // step, the whole halo of hc+1: leave only younger DMAs in
@@ -424,13 +475,18 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 if (D == 1)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 else
-                    wait_vmcnt(sg == SPC - 1 ? nw : nw + nh);
+                    wait_vmcnt(G::allowed(sg, part, HALVES));
                 __builtin_amdgcn_s_barrier();
-            }
+            };
+            [&]<int... SG>(std::integer_sequence<int, SG...>) {
+                (step(std::integral_constant<int, SG>{}), ...);
+            }(std::make_integer_sequence<int, SPC>{});
         };
         half_chunk(std::integral_constant<int, 0>{});
         if constexpr (HALVES == 2) half_chunk(std::integral_constant<int, 1>{});
     }
+    // the last steps issued dummy DMAs (past the end) into LDS the epilogue reuses
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---------------- epilogue ----------------
     const float inv = 1.0f / sxw;  // 2^-k: exact
