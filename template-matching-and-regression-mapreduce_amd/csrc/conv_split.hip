@@ -244,15 +244,32 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int l16 = lane & 15, kg = lane >> 4;
     const int wn = wave % WNS, wpix = wave / WNS;
 
-    // XCD-aware bijective remap (the 8 XCDs take blocks round robin): the NT
-    // channel tiles of a pixel tile run back to back on one XCD and share its
-    // halo through L2.
+    // XCD-aware bijective remap (the 8 XCDs take blocks round robin): L is
+    // contiguous per XCD, so consecutive L run concurrently on one XCD.
     const int nblk = gridDim.x, orig = blockIdx.x;
     const int q8 = nblk >> 3, r8 = nblk & 7, xcd = orig & 7;
     const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    const int nt = L % a.NT;
-    const int rest = L / a.NT;
-    const int mt = rest % a.MT, u = rest / a.MT;
+    int nt, mt, u;
+    {
+        constexpr int PXG = 8, NG = 4;  // one XCD wave of 32 blocks = 8 pixel tiles x 4 channel tiles
+        const int per_unit = a.NT * a.MT;
+        u = L / per_unit;
+        const int r = L - u * per_unit;
+        if (a.MT % PXG == 0 && a.NT % NG == 0) {
+            // pixel tiles in groups of 8; for each group the channel tiles in
+            // groups of 4: the 32 co-resident blocks of an XCD share 4 weight
+            // slabs and 8 halos through its L2, and a group's halos stay
+            // there while its 4 channel groups pass
+            const int gsz = PXG * a.NT;
+            const int pg = r / gsz, r2 = r - pg * gsz;
+            const int ng = r2 / (PXG * NG), r3 = r2 - ng * (PXG * NG);
+            mt = pg * PXG + r3 / NG;
+            nt = ng * NG + r3 % NG;
+        } else {
+            nt = r % a.NT;
+            mt = r / a.NT;
+        }
+    }
     const int ty0 = (mt / a.TXN) * TH, tx0 = (mt % a.TXN) * TW;
     const int img = a.unit_image ? a.unit_image[u] : u;
     const int NC = a.NC0 + a.NC1;
