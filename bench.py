@@ -198,7 +198,7 @@ def main():
                            % ("bf16" if prec == "bf16" else "f16"))
             flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
                            "(%s; the fp half runs once per image in tmr_split_conv_store and is "
-                           "shared by its exemplars; K=1024*9 when E=1)"
+                           "shared by its exemplars; unshared (E=1): K=(256+512)*9, the fp half folded through input_proj)"
                            % (terms, "fp32-grade 3-term fp16 split: hi*hi + lo*hi + hi*lo"
                               if terms == 3 else "one %s term" % prec))
         elif algo == "wino":

@@ -192,3 +192,76 @@ def test_map_phase_gpu_with_detections():
             dets += bo[0].shape[0]
         assert rec[s, 5] == cnt and rec[s, 6] == dets
         np.testing.assert_allclose(rec[s, 1:5], sums, rtol=1e-5, atol=1e-6)
+
+
+# ---------------------------------------------------------------- feature cache (§8f f3)
+def _feature_tree(root, shards, seed=40, C=8, h=6):
+    """The reference mapper's output layout: <root>/<Category>/<tar stem>/<image>.npy [1,C,h,h]."""
+    rng = np.random.default_rng(seed)
+    for si, name in enumerate(shards):
+        stem = name.replace(".tar", "")
+        d = os.path.join(root, mr.category_of(stem), stem)
+        os.makedirs(d, exist_ok=True)
+        for j in range(int(rng.integers(0, 4))):  # 0..3 images (0: the tar emits no line)
+            np.save(os.path.join(d, f"img_{j}.npy"),
+                    synth.sam_features(100 * si + j, 1, C, h, h))
+
+
+def test_npy_feature_source_map(tmp_path):
+    shards = SHARDS[:7]
+    _feature_tree(str(tmp_path), shards)
+    src = mr.NpyFeatureSource(str(tmp_path), shards, torch.device("cpu"), 2, 3, 5, 0,
+                              exemplars={"Normal_1/img_0": [[0.1, 0.1, 0.3, 0.3]]})
+    assert len(src.counts) == len(shards) and sum(src.counts) == len(src.files)
+    rec = mr.run_mapper(shards, src.counts, 0, 1, src, _cpu_stats, None, batch=2)
+    for s, name in enumerate(shards):
+        stem = name.replace(".tar", "")
+        fs = sorted(os.listdir(os.path.join(str(tmp_path), mr.category_of(stem), stem)))
+        stats = [oracle.mapper_stats(np.load(os.path.join(str(tmp_path), mr.category_of(stem), stem, f)))
+                 for f in fs]
+        sums, cnt = oracle.mapper_tar_sums(stats)
+        assert rec[s, 5] == cnt and list(rec[s, 1:5]) == sums
+    lines = mr.mapper_lines(shards, rec)
+    assert len(lines) == sum(1 for c in src.counts if c > 0)  # empty tars emit nothing (mapper.py:127)
+    i = src.keys.index("Normal_1/img_0")
+    _, ex = src([i])
+    np.testing.assert_array_equal(ex[0], np.float32([[0.1, 0.1, 0.3, 0.3]] * 2))
+
+
+def test_load_weights_lightning_prefix(tmp_path):
+    P = oracle.reference_weights(0, cin=8, emb=8)
+    sd = {"model." + k: v for k, v in P.items()}
+    sd["model.encoder.backbone.w"] = torch.zeros(2)
+    torch.save({"state_dict": sd, "epoch": 3}, str(tmp_path / "c.ckpt"))
+    got = mr.load_weights(str(tmp_path / "c.ckpt"), torch.device("cpu"))
+    assert set(got) == set(P)
+    for k in P:
+        assert torch.equal(got[k], P[k].float())
+
+
+@pytest.mark.gpu
+def test_stream_cli_on_feature_tree(tmp_path, capsys):
+    """stream.py main() on the mapper's feature tree with a checkpoint: the
+    reducer table equals the CPU oracle's (statistics within the kernel's
+    fp32-rounding tolerance at 4 decimals, counts exact)."""
+    shards = SHARDS[:6]
+    root = tmp_path / "feat"
+    _feature_tree(str(root), shards, C=32, h=8)
+    P = oracle.reference_weights(0, cin=32, emb=32)
+    torch.save(P, str(tmp_path / "w.pt"))
+    lst = tmp_path / "list.txt"
+    lst.write_text("".join(s + "\n" for s in shards))
+    mr.main(["--list", str(lst), "--features-root", str(root), "--ckpt", str(tmp_path / "w.pt"),
+             "--exemplars", "2", "--kmax", "5", "--detections", "--mapper-out", str(tmp_path / "m.txt")])
+    out = capsys.readouterr().out
+    src = mr.NpyFeatureSource(str(root), shards, torch.device("cpu"), 2, 3, 5, 0)
+    rec = mr.run_mapper(shards, src.counts, 0, 1, src, _cpu_stats, None, batch=64)
+    lines = open(str(tmp_path / "m.txt")).read().splitlines()
+    ref_lines = mr.hadoop_sort(mr.mapper_lines(shards, rec))
+    assert [l.split("\t")[0] for l in lines] == [l.split("\t")[0] for l in ref_lines]
+    for l, r in zip(lines, ref_lines):
+        got = [float(v) for v in l.split("\t")[1].split(",")]
+        exp = [float(v) for v in r.split("\t")[1].split(",")]
+        assert got[4] == exp[4] and got[2] == exp[2] and got[3] == exp[3]  # count, max, sparsity exact
+        np.testing.assert_allclose(got[:2], exp[:2], rtol=1e-6, atol=1e-6)
+    assert out.splitlines()[0].startswith("CATEGORY")
