@@ -20,10 +20,14 @@
 //
 // Operands live in HBM in MFMA-ready 16-bit layouts written by the pack
 // kernels below.  Activations: per 32-channel chunk and "half" (F16X3: hi,
-// lo; one-term modes: one half) a 64-B record per pixel, zero-padded to whole
-// tiles plus the kxk halo, so the kernel never masks a load.  Weights: per
-// tap and chunk a record per output channel, [wh ch0-31][wl ch0-31] (128 B,
-// F16X3) or [w ch0-31] (64 B).
+// lo; one-term modes: one half) a 64-B record per pixel (4 16-B pieces of 8
+// channels), zero-padded to whole tiles plus the kxk halo, so the kernel
+// never masks a load.  Weights: per tap and chunk a record per output
+// channel, [wh ch0-31][wl ch0-31] (128 B, F16X3) or [w ch0-31] (64 B).  Both
+// are stored PLANAR (piece q of every record contiguous), which is also the
+// LDS image layout: each 1-KB LDS-DMA wave instruction reads 1 KB of
+// contiguous HBM (a record-major layout reads 16 B of every 64-128 B line
+// per instruction: 4-8x the L2/TA line traffic, measured ~6% of the kernel).
 //
 // The F16X3 K loop alternates two half-chunk kinds over the same 32
 // channels: "hi" (halo xh; 2 MFMAs per tile: wh.xh + wl.xh) and "lo" (halo
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
-        return ((ty0 + hy) * a.Wp + (tx0 + hx)) * XREC + q * 16;
+        return ((q * a.Hp + ty0 + hy) * a.Wp + (tx0 + hx)) * 16;  // planar records: piece q plane
     };
     // Buffer descriptors (SGPRs) over this block's source slabs and weights:
     // every DMA is base + uniform soffset + a 32-bit per-lane voffset, so the
@@ -309,11 +313,13 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     };
     // weights of flat step g: half-chunk g / SPC (hi: wh and wl planes, lo:
     // wh only), taps TPS*(g % SPC)...; instruction i of the step = tap i/IPT,
-    // plane (i%IPT)/2, channels 64*((i%IPT)&1) + lane.  Returns the count.
+    // plane (i%IPT)/2, channels 64*((i%IPT)&1) + lane: 1 KB contiguous in the
+    // planar HBM layout [tap][chunk][plane][Npad][16 B].
     const uint32_t tapstride = (uint32_t)NC * a.Npad * WREC;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(a.wp + (size_t)nt * BM * WREC), (short)0, T * tapstride - nt * BM * WREC, 0x00020000);
-    const int wlane = lane * WREC;
+        (void *)a.wp, (short)0, T * tapstride, 0x00020000);
+    const int wlane = lane * 16;
+    const uint32_t wnt = (uint32_t)nt * BM * 16;
     // this wave's weight instruction m of flat step g, whose shape (lo, taps)
     // the caller knows at compile time: ipt instructions per tap, every wave
     // issuing the same count (ipt is a multiple of NWAVES).  g == S (past the
@@ -321,11 +327,11 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     auto w_dma1 = [&](int g, int ipt, int m) {
         const int hc = g / SPC, t0 = (g - hc * SPC) * TPS;
         const int c = hc / HALVES;
-        const uint32_t src = (uint32_t)t0 * tapstride + (uint32_t)c * a.Npad * WREC;
+        const uint32_t src = (uint32_t)t0 * tapstride + (uint32_t)c * a.Npad * WREC + wnt;
         char *dst = Ws + (g % NWB) * WB;
         const int i = wave + NWAVES * m;
         const int tl = i / ipt, wi = i - tl * ipt;
-        const uint32_t so = src + (uint32_t)tl * tapstride + ((wi & 1) * 64 * WREC + (wi >> 1) * 16);
+        const uint32_t so = src + (uint32_t)tl * tapstride + (uint32_t)(wi >> 1) * a.Npad * 16 + (wi & 1) * 64 * 16;
         buffer_lds16(wr, (lds_ptr_t)(dst + tl * WB1 + wi * 1024), wlane, so);
     };
 
@@ -662,7 +668,7 @@ __global__ void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4, unsi
     if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// Activation records: value v(s, ch, y, x) -> [S][NCc*HALVES][Hp][Wp][64 B],
+// Activation records: value v(s, ch, y, x) -> [S][NCc*HALVES][4 pieces][Hp][Wp][16 B],
 // padded (yp, xp) holding v at (yp - ks/2, xp - ks/2), zero outside.  One
 // thread per (s, chunk, yp, xp) writes the chunk's hi (and lo) record.
 // MODE 0: v = x[s][ch][y][x]; MODE 1: v = [up2x(f) or f; 1] from the SAM
@@ -705,13 +711,15 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
     }
     typename Prec<PREC>::V hi[P], lo[P];
     split_record<PREC>(v, sc, hi, lo);
+    // planar: [s][chunk][half][piece q][Hp][Wp] 16-B pieces (the conv's
+    // LDS-DMA reads 64 consecutive pieces of one plane per instruction)
     const size_t plane = (size_t)Hp * Wp;
-    typename Prec<PREC>::V *o = out + (((size_t)s * NCc + c) * HALVES * plane + (size_t)yp * Wp + xp) * P;
+    typename Prec<PREC>::V *o = out + ((size_t)s * NCc + c) * HALVES * P * plane + (size_t)yp * Wp + xp;
 #pragma unroll
-    for (int q = 0; q < P; ++q) o[q] = hi[q];
+    for (int q = 0; q < P; ++q) o[q * plane] = hi[q];
     if (HALVES == 2) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) o[plane * P + q] = lo[q];
+        for (int q = 0; q < P; ++q) o[(P + q) * plane] = lo[q];
     }
 }
 
@@ -739,7 +747,7 @@ __global__ void fold_proj_kernel(const float *__restrict__ wd, int N, int Cw, in
     out[i] = (float)acc;
 }
 
-// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][Npad][WREC]; the src0
+// w [N][C0+C1][ks][ks] fp32 -> [ks*ks][NC0+NC1][WREC/16 planes][Npad][16 B]; the src0
 // and src1 channel ranges are padded to whole 32-channel chunks separately.
 template <int PREC>
 __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1, int ks, int NC0,
@@ -772,13 +780,14 @@ __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1,
     }
     typename Prec<PREC>::V hi[P], lo[P];
     split_record<PREC>(v, sc, hi, lo);
+    // planar: [tap][chunk][plane (wh pieces, then wl pieces)][Npad] 16-B pieces
     constexpr int NP = Prec<PREC>::WREC / 16;
-    typename Prec<PREC>::V *o = out + i * NP;
+    typename Prec<PREC>::V *o = out + ((size_t)tap * NC + c) * NP * Npad + n;
 #pragma unroll
-    for (int q = 0; q < P; ++q) o[q] = hi[q];
+    for (int q = 0; q < P; ++q) o[(size_t)q * Npad] = hi[q];
     if (NP == 8) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) o[P + q] = lo[q];
+        for (int q = 0; q < P; ++q) o[(size_t)(P + q) * Npad] = lo[q];
     }
 }
 
