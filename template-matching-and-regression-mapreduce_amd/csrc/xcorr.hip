@@ -6,17 +6,23 @@
 // One workgroup per (band of RB output rows, channel, image): the band's
 // input rows of the image's fp plane are staged once in LDS and reused by
 // every exemplar unit of that image (the reference's per-exemplar forwards
-// re-read it E times).  Each lane owns a 4x4 block of outputs and slides the
+// re-read it E times).  Each lane owns a 2x8 block of outputs and slides the
 // template over register windows (compile-time template width, wave-uniform
-// taps), ~11 FMAs per LDS read at 15x15.  The divide is an IEEE fp32 division
-// by fl32(h*w) exactly like the reference's `/ (h*w + 1e-14)`.
+// taps from SGPRs, v_pk_fma_f32 on output pairs).  Measured at config B
+// (kbench_xcorr): 4x4 scalar 7.31 ms, 4x4 packed 7.47, 2x8 packed 7.37; at
+// config E (k <= 31) 12.9 / 10.5 / 10.4 ms.  Not VALU-bound: without stores
+// and border zeroing it is 5.4 ms (1.6 ms of packed FMA issue); taps staged
+// in LDS instead of SGPRs: 9.1 ms.  The divide by fl32(h*w) is correctly
+// rounded (div_cr), bit-identical to the reference's `/ (h*w + 1e-14)`.
 #include "tmr_common.h"
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 constexpr int NT = 256;
-constexpr int RY = 4;  // output rows per lane
-constexpr int RX = 4;  // output cols per lane
+constexpr int RY = 2;  // output rows per lane
+constexpr int RX = 8;  // output cols per lane
 constexpr int XSLACK = 16;  // zeroed floats past the last LDS row (16-B row reads over-read)
 
 struct XArgs {
@@ -32,20 +38,45 @@ struct XArgs {
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
 };
 
-// acc[r][q] += sum_{i<h, j<KW} X[r0 + r + i][x0 + q + j] * T[i][j]
+// x / d correctly rounded (= the reference's IEEE `/ (h*w + 1e-14)` in fp32)
+// from rd = RN(1/d): q = RN(x rd), then one fma residual step (Markstein).
+// Checked bit-exact against true division on 4.2e8 normal-range x for every
+// odd h, w <= 31 (oracle-free host check); 3 VALU ops instead of the ~10 of
+// the v_div_scale/fmas/fixup sequence.
+__device__ __forceinline__ float div_cr(float x, float d, float rd) {
+    const float q = x * rd;
+    const float r = fmaf(-q, d, x);
+    return fmaf(r, rd, q);
+}
+
+// acc[r][q] += sum_{i<h, j<KW} X[r0 + r + i][x0 + q + j] * T[i][j] as
+// v_pk_fma_f32 on output pairs (q, q+1) with the
+// wave-uniform tap broadcast from an SGPR (op_sel), two outputs per VALU
+// issue.  A tap at even j reads the row's even-aligned register pairs
+// (x[j], x[j+1]); at odd j the odd pairs (x[j], x[j+1]) built once per row
+// (one v_pk_mov_b32 each).
 template <int KW>
-__device__ __forceinline__ void corr_block(const float *xs, int W, int x0, int r0,
-                                           const float *__restrict__ tc, int h,
-                                           float (&acc)[RY][RX]) {
-    constexpr int NV = (KW + RX - 1 + 3) / 4;  // 16-B LDS reads per row (W % 4 == 0: aligned)
+__device__ __forceinline__ void corr_block_pk(const float *xs, int W, int x0, int r0,
+                                              const float *__restrict__ tc, int h,
+                                              float (&acc)[RY][RX]) {
+    constexpr int NV = (KW + RX - 1 + 3) / 4;
+    constexpr int NO = (KW >= 2 ? (KW - 2) / 2 : 0) + RX / 2;  // odd pairs (x[2m+1], x[2m+2]) used
+    f32x2 pa[RY][RX / 2];
+#pragma unroll
+    for (int r = 0; r < RY; ++r)
+#pragma unroll
+        for (int q = 0; q < RX / 2; ++q) pa[r][q] = f32x2{acc[r][2 * q], acc[r][2 * q + 1]};
     for (int ii = 0; ii < RY + h - 1; ++ii) {
         const float4 *xr = reinterpret_cast<const float4 *>(xs + (r0 + ii) * W + x0);
-        float xv[4 * NV];
+        f32x2 xe[2 * NV], xo[NO];
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const float4 v4 = xr[j];
-            xv[4 * j] = v4.x; xv[4 * j + 1] = v4.y; xv[4 * j + 2] = v4.z; xv[4 * j + 3] = v4.w;
+            xe[2 * j] = f32x2{v4.x, v4.y};
+            xe[2 * j + 1] = f32x2{v4.z, v4.w};
         }
+#pragma unroll
+        for (int m = 0; m < NO; ++m) xo[m] = f32x2{xe[m].y, xe[m + 1].x};
 #pragma unroll
         for (int r = 0; r < RY; ++r) {
             const int i = ii - r;
@@ -54,11 +85,22 @@ __device__ __forceinline__ void corr_block(const float *xs, int W, int x0, int r
 #pragma unroll
             for (int j = 0; j < KW; ++j) {
                 const float t = tr[j];
+                const f32x2 tt = {t, t};
 #pragma unroll
-                for (int q = 0; q < RX; ++q) acc[r][q] = fmaf(xv[q + j], t, acc[r][q]);
+                for (int q = 0; q < RX / 2; ++q) {
+                    const f32x2 xv2 = (j & 1) ? xo[(j >> 1) + q] : xe[(j >> 1) + q];
+                    pa[r][q] = __builtin_elementwise_fma(xv2, tt, pa[r][q]);
+                }
             }
         }
     }
+#pragma unroll
+    for (int r = 0; r < RY; ++r)
+#pragma unroll
+        for (int q = 0; q < RX / 2; ++q) {
+            acc[r][2 * q] = pa[r][q].x;
+            acc[r][2 * q + 1] = pa[r][q].y;
+        }
 }
 
 // generic width (templates wider than 31)
@@ -86,7 +128,7 @@ __device__ void corr_dispatch(int w, const float *xs, int W, int x0, int r0, con
         return;
     }
     switch (w) {
-#define TMR_W(K) case K: corr_block<K>(xs, W, x0, r0, tc, h, acc); break;
+#define TMR_W(K) case K: corr_block_pk<K>(xs, W, x0, r0, tc, h, acc); break;
         TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
         TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
 #undef TMR_W
@@ -137,16 +179,21 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
         const int nv = max(yz - ya, 0);
         const float sc = a.squeeze ? 1.0f : *a.scale;
         const float denom = (float)(h * w);
+        const float rden = 1.0f / denom;  // correctly rounded reciprocal
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
                               : outp + ((size_t)u * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
-        if (!a.squeeze) {  // zero border of this band
-            for (int e = threadIdx.x; e < (yb1 - yb0) * W; e += NT) {
-                const int yo = yb0 + e / W, xo = e % W;
+        if (!a.squeeze) {  // zero border of this band ((yo, xo) stepped, no per-element division)
+            int yo = yb0 + (int)threadIdx.x / W, xo = (int)threadIdx.x % W;
+            const int sy = NT / W, sx = NT % W;
+            for (; yo < yb1;) {
                 if (!(yo >= ya && yo < yz && xo >= pw && xo < pw + Wo)) {
                     op[(size_t)yo * W + xo] = 0.0f;
                     if (rp) rp[(size_t)yo * W + xo] = 0.0f;
                 }
+                yo += sy;
+                xo += sx;
+                if (xo >= W) { xo -= W; ++yo; }
             }
         }
         const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
@@ -172,7 +219,7 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
                 for (int q = 0; q < RX; ++q) {
                     if (x0 + q >= Wo) break;
                     const size_t o = (size_t)(ya + r0 + r) * W + x0 + q + pw;
-                    const float v = (acc[r][q] / denom) * sc;
+                    const float v = div_cr(acc[r][q], denom, rden) * sc;
                     op[o] = v;
                     vmax = fmaxf(vmax, fabsf(v));
                     if (rp) rp[o] = v > 0.0f ? v : 0.0f;
