@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--E", type=int, default=3)
     ap.add_argument("--kmax", type=int, default=15)
+    ap.add_argument("--kmin", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, H = a.images, 512, 128
@@ -35,7 +36,7 @@ def main():
     eng = tmr.TMREngine(P, tmr.PathConfig())
     g = torch.Generator(device=dev).manual_seed(0)
     fp = torch.randn((B, C, H, H), device=dev, generator=g)
-    ex, ks = synth.exemplar_set(1, B, a.E, H, H, 3, a.kmax)
+    ex, ks = synth.exemplar_set(1, B, a.E, H, H, a.kmin, a.kmax)
     ui = np.repeat(np.arange(B), a.E)
     boxes = ex.reshape(-1, 4)
     flops = 0.0
@@ -53,7 +54,7 @@ def main():
         ts.append(s.elapsed_time(e))
     ms = float(np.median(ts))
     out_bytes = B * a.E * C * H * H * 4
-    print(json.dumps({"images": B, "E": a.E, "ms": round(ms, 3), "gflop": round(flops / 1e9, 1),
+    print(json.dumps({"images": B, "E": a.E, "k": [a.kmin, a.kmax], "ms": round(ms, 3), "gflop": round(flops / 1e9, 1),
                       "tflops": round(flops / ms / 1e9, 1), "frac_valu": round(flops / ms / 1e9 / 157.3, 3),
                       "hbm_gbps_out": round(out_bytes / ms / 1e6, 1)}))
 

@@ -3,6 +3,9 @@
 // template area, the zero pad back to HxW and the learned scale:
 //   models/template_matching.py:23-41 (cross_correlation), :97 (f * scale).
 //
+// Two kernels, same results: xcorr_rows_kernel (rows 16-B aligned, templates
+// <= 31 wide: the engine's shapes) and xcorr_kernel (any shape).
+//
 // One workgroup per (band of RB output rows, channel, image): the band's
 // input rows of the image's fp plane are staged once in LDS and reused by
 // every exemplar unit of that image (the reference's per-exemplar forwards
@@ -12,7 +15,10 @@
 // (kbench_xcorr): 4x4 scalar 7.31 ms, 4x4 packed 7.47, 2x8 packed 7.37; at
 // config E (k <= 31) 12.9 / 10.5 / 10.4 ms.  Not VALU-bound: without stores
 // and border zeroing it is 5.4 ms (1.6 ms of packed FMA issue); taps staged
-// in LDS instead of SGPRs: 9.1 ms.  The divide by fl32(h*w) is correctly
+// in LDS instead of SGPRs: 9.1 ms.  xcorr_rows_kernel (aligned 16-B row
+// stores, border in the tiles) then takes config B to 6.66 ms and k = 3 from
+// 5.44 to 3.66 ms (k = 15: 10.7 -> 11.3, config E 10.4 -> 11.7: the border
+// tiles' compute).  The divide by fl32(h*w) is correctly
 // rounded (div_cr), bit-identical to the reference's `/ (h*w + 1e-14)`.
 #include "tmr_common.h"
 
@@ -36,6 +42,7 @@ struct XArgs {
     float *work;
     unsigned *out_absmax;  // nullable [TMR_ABSMAX_SLOTS]: slot-wise atomicMax of |out|
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
+    int HG;                          // rows kernel: max template height / 2
 };
 
 // x / d correctly rounded (= the reference's IEEE `/ (h*w + 1e-14)` in fp32)
@@ -242,6 +249,151 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// Row-tiled variant (W % 4 == 0, templates up to 31 wide): lane tiles cover
+// the WHOLE output band, zero border included, in 4x4 tiles aligned to the
+// output columns, so every output row leaves as one 16-B store per lane (a
+// wave writes 1 KB contiguous) and no separate border pass exists.  The band
+// is staged with zero pads (PADL columns left, PADR right, zero rows above
+// and below the image), so a tile's input window is always in range; border
+// outputs are computed from the pads and masked to 0.  The window of output
+// columns c0..c0+3 starts at input column c0 - KW/2, whose misalignment
+// OFF = (-(KW/2)) mod 4 is a compile-time constant of the width
+// specialisation: reads are aligned b128, pairs are picked at compile time.
+constexpr int PADL = 20;  // >= 15 + 3 (max half-width + OFF), multiple of 4
+constexpr int PADR = 24;  // covers the window over-read past column W
+constexpr int TRY = 4, TRX = 4;
+
+template <int KW>
+__device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, int lcol0,
+                                          const float *__restrict__ tc, int h, f32x2 (&pa)[TRY][2]) {
+    constexpr int OFF = (4 - ((KW / 2) & 3)) & 3;
+    constexpr int NV = (OFF + KW + TRX + 3) / 4;   // b128 reads per row (+1 float for odd pairs)
+    constexpr int NO = (OFF + KW + TRX - 2) / 2;   // odd pairs (x[2m+1], x[2m+2])
+    for (int ii = 0; ii < TRY + h - 1; ++ii) {
+        const float4 *xr = reinterpret_cast<const float4 *>(xs + (lrow0 + ii) * WS + lcol0);
+        f32x2 xe[2 * NV], xo[NO];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const float4 v4 = xr[j];
+            xe[2 * j] = f32x2{v4.x, v4.y};
+            xe[2 * j + 1] = f32x2{v4.z, v4.w};
+        }
+#pragma unroll
+        for (int m = 0; m < NO; ++m) xo[m] = f32x2{xe[m].y, xe[m + 1].x};
+#pragma unroll
+        for (int r = 0; r < TRY; ++r) {
+            const int i = ii - r;
+            if (i < 0 || i >= h) continue;  // wave-uniform
+            const float *tr = tc + i * KW;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const float t = tr[j];
+                const f32x2 tt = {t, t};
+#pragma unroll
+                for (int q = 0; q < TRX / 2; ++q) {
+                    const int s0 = 2 * q + j + OFF;  // compile-time after unrolling
+                    const f32x2 xv2 = (s0 & 1) ? xo[s0 >> 1] : xe[s0 >> 1];
+                    pa[r][q] = __builtin_elementwise_fma(xv2, tt, pa[r][q]);
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__restrict__ tmpl,
+                                                       float *__restrict__ outp) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    const int band = blockIdx.x, c = blockIdx.y, img = blockIdx.z;
+    const int H = a.H, W = a.W, WS = W + PADL + PADR;
+    const int u_beg = __builtin_amdgcn_readfirstlane(a.img_units[img]);
+    const int u_end = __builtin_amdgcn_readfirstlane(a.img_units[img + 1]);
+    if (u_beg >= u_end) return;
+    const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
+    const int hg = a.HG;  // half of the largest template height: LDS row 0 = image row yb0 - hg
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    // stage rows [yb0 - hg, yb0 - hg + LR) with zero pads (rows outside the image: zeros)
+    const int W4 = W / 4, WS4 = WS / 4;
+    float4 *xs4 = reinterpret_cast<float4 *>(xs);
+    for (int e = threadIdx.x; e < a.LR * WS4; e += NT) {
+        const int lr = e / WS4, cc = e - lr * WS4 - PADL / 4;
+        const int yy = yb0 - hg + lr;
+        float4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (yy >= 0 && yy < H && cc >= 0 && cc < W4)
+            v = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        xs4[e] = v;
+    }
+    __syncthreads();
+
+    const size_t plane = (size_t)H * W;
+    const int nbx = W / TRX, nby = (yb1 - yb0 + TRY - 1) / TRY;
+    float vmax = 0.0f;
+    for (int u = u_beg; u < u_end; ++u) {
+        const tmr_unit_t &un = a.units[u];
+        const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
+        const int ph = h / 2, pw = w / 2;
+        const int Ho = H - h + 1, Wo = W - w + 1;
+        const float sc = a.squeeze ? 1.0f : *a.scale;
+        const float denom = (float)(h * w);
+        const float rden = 1.0f / denom;  // correctly rounded reciprocal
+        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
+                              : outp + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
+        for (int task = threadIdx.x; task < nbx * nby; task += NT) {
+            const int c0 = (task % nbx) * TRX, y0 = yb0 + (task / nbx) * TRY;
+            f32x2 pa[TRY][2];
+#pragma unroll
+            for (int r = 0; r < TRY; ++r) pa[r][0] = pa[r][1] = f32x2{0.0f, 0.0f};
+            const int lrow0 = y0 - yb0 + hg - ph;
+            const int lcol0 = PADL + c0 - pw - ((4 - (pw & 3)) & 3);
+            // tiles wholly in the border rows or columns only store zeros
+            const bool live = y0 + TRY > ph && y0 < ph + Ho && c0 + TRX > pw && c0 < pw + Wo;
+            if (live) switch (w) {
+#define TMR_W(K) case K: corr_tile<K>(xs, WS, lrow0, lcol0, tc, h, pa); break;
+                TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
+                TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
+#undef TMR_W
+                default: break;  // even widths never reach this kernel (host check)
+            }
+#pragma unroll
+            for (int r = 0; r < TRY; ++r) {
+                const int y = y0 + r;
+                if (y >= yb1) break;
+                const bool vy = y >= ph && y < ph + Ho;
+                float v[TRX];
+#pragma unroll
+                for (int q = 0; q < TRX; ++q) {
+                    const int cx = c0 + q;
+                    const float acc = (q & 1) ? pa[r][q >> 1].y : pa[r][q >> 1].x;
+                    v[q] = (vy && cx >= pw && cx < pw + Wo) ? div_cr(acc, denom, rden) * sc : 0.0f;
+                    vmax = fmaxf(vmax, fabsf(v[q]));
+                }
+                const size_t o = (size_t)y * W + c0;
+                *reinterpret_cast<float4 *>(op + o) = float4{v[0], v[1], v[2], v[3]};
+                if (rp)
+                    *reinterpret_cast<float4 *>(rp + o) =
+                        float4{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f), fmaxf(v[2], 0.0f), fmaxf(v[3], 0.0f)};
+            }
+        }
+    }
+    if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
+        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+        __syncthreads();  // xs is free: every unit's reads are done
+        if ((threadIdx.x & 63) == 0) xs[threadIdx.x >> 6] = vmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float m = xs[0];
+            for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, xs[w]);
+            const unsigned slot = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) %
+                                  TMR_ABSMAX_SLOTS;
+            atomicMax(a.out_absmax + slot, __float_as_uint(m));
+        }
+    }
+}
+
 // squeeze (template_matching.py:34-35): sum over channels, pad, scale
 __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_unit_t *__restrict__ units,
                                      int U, int C, int H, int W, const float *__restrict__ scale,
@@ -282,9 +434,13 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
-    // LDS rows: band + template halo + RY slack rows for partial 4-row blocks
-    const int max_rows = (150 * 1024) / (4 * W) - 1;
-    const int RB = min(32, max_rows - (max_ht - 1) - RY);
+    // row-tiled kernel when rows are 16-B aligned and templates fit its
+    // width specialisations (template sizes are odd, template_matching.py:66-73)
+    const bool rows = (W % 4) == 0 && max_wt <= 31;
+    const int WS = rows ? W + PADL + PADR : W;
+    // LDS rows: band + template halo + slack rows for partial 4-row tiles
+    const int max_rows = (150 * 1024) / (4 * WS) - 1;
+    const int RB = min(32, max_rows - (max_ht - 1) - (rows ? TRY + 3 : RY));
     if (RB < 1) return TMR_E_UNSUPPORTED;
     XArgs a;
     a.f = f;
@@ -301,16 +457,21 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     a.W = W;
     a.RB = RB;
     a.squeeze = squeeze;
-    a.LR = RB + max_ht - 1 + RY;
-    const size_t lds = ((size_t)a.LR * W + XSLACK) * sizeof(float);
+    a.LR = rows ? RB + max_ht + 3 : RB + max_ht - 1 + RY;
+    a.HG = max_ht / 2;
+    const size_t lds = rows ? (size_t)a.LR * WS * sizeof(float)
+                            : ((size_t)a.LR * W + XSLACK) * sizeof(float);
+    const void *kfn = rows ? (const void *)xcorr_rows_kernel : (const void *)xcorr_kernel;
     hipStream_t s = tmr_stream(stream);
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)xcorr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
+        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return TMR_E_HIP;
     TMR_REQUIRE(C < 65536 && B < 65536);
     dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
-    hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
+    if (rows)
+        hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
+    else
+        hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
     TMR_CHECK_LAUNCH();
     if (squeeze) {
         int64_t tot = (int64_t)U * H * W;
