@@ -20,3 +20,4 @@ run B_write -- WRITE_SIZE || exit 1
 run B_core -- GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS || exit 1
 run C_fetch --config C -- FETCH_SIZE || exit 1
 run C_write --config C -- WRITE_SIZE || exit 1
+python profiles/pmc_assemble.py gpurun_out/pmc "${ROUND:-current}" gpurun_out/decoder_pmc.json > gpurun_out/pmc_assemble.log 2>&1 || exit 1

@@ -18,21 +18,29 @@ import sys
 
 
 def collect(kernel, paths):
-    vals = collections.defaultdict(list)
-    dur = []
+    """Counter values and durations of the matching launches with the
+    largest grid (a kernel's small side launches, e.g. the one-off bias-plane
+    launch of split_conv_kernel<3,0,0>, are left out of the averages)."""
+    rows = []
     for p in paths:
         files = glob.glob(os.path.join(p, "**", "*counter_collection.csv"), recursive=True) \
             if os.path.isdir(p) else [p]
         for f in files:
-            seen = set()
             for row in csv.DictReader(open(f)):
-                if kernel not in row["Kernel_Name"]:
-                    continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-                key = (f, row["Dispatch_Id"])
-                if key not in seen:
-                    seen.add(key)
-                    dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+                if kernel in row["Kernel_Name"]:
+                    rows.append((f, row))
+    gmax = max((int(r["Grid_Size"]) for _, r in rows), default=0)
+    vals = collections.defaultdict(list)
+    dur = []
+    seen = set()
+    for f, row in rows:
+        if int(row["Grid_Size"]) != gmax:
+            continue
+        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        key = (f, row["Dispatch_Id"])
+        if key not in seen:
+            seen.add(key)
+            dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
     return vals, dur
 
 
