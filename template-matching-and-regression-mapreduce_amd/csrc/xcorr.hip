@@ -18,7 +18,10 @@
 // in LDS instead of SGPRs: 9.1 ms.  xcorr_rows_kernel (aligned 16-B row
 // stores, border in the tiles) then takes config B to 6.66 ms and k = 3 from
 // 5.44 to 3.66 ms (k = 15: 10.7 -> 11.3, config E 10.4 -> 11.7: the border
-// tiles' compute).  The divide by fl32(h*w) is correctly
+// tiles' compute); staging loads batched 8 per thread before the LDS writes:
+// k = 3 2.98 ms, k = 5 5.59 -> 3.58 ms, config B 6.53 ms.  (Whole-template
+// taps preloaded for 3x3: no change; for 5x5 the 25 taps spill SGPRs.)  The
+// divide by fl32(h*w) is correctly
 // rounded (div_cr), bit-identical to the reference's `/ (h*w + 1e-14)`.
 #include "tmr_common.h"
 
@@ -302,7 +305,8 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
 }
 
 __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__restrict__ tmpl,
-                                                       float *__restrict__ outp) {
+                                                       float *__restrict__ outp,
+                                                       const tmr_unit_t *__restrict__ units) {
     extern __shared__ __attribute__((aligned(16))) float xs[];
     const int band = blockIdx.x, c = blockIdx.y, img = blockIdx.z;
     const int H = a.H, W = a.W, WS = W + PADL + PADR;
@@ -312,16 +316,27 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
     const int hg = a.HG;  // half of the largest template height: LDS row 0 = image row yb0 - hg
     const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    const float sc = a.squeeze ? 1.0f : *a.scale;  // read once, before any store
     // stage rows [yb0 - hg, yb0 - hg + LR) with zero pads (rows outside the image: zeros)
-    const int W4 = W / 4, WS4 = WS / 4;
+    // SU loads per thread in flight before any LDS write (a load -> ds_write
+    // loop waits out one global-load latency per element)
+    constexpr int SU = 8;
+    const int W4 = W / 4, WS4 = WS / 4, n4 = a.LR * WS4;
     float4 *xs4 = reinterpret_cast<float4 *>(xs);
-    for (int e = threadIdx.x; e < a.LR * WS4; e += NT) {
-        const int lr = e / WS4, cc = e - lr * WS4 - PADL / 4;
-        const int yy = yb0 - hg + lr;
-        float4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (yy >= 0 && yy < H && cc >= 0 && cc < W4)
-            v = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
-        xs4[e] = v;
+    for (int e0 = threadIdx.x; e0 < n4; e0 += NT * SU) {
+        float4 v[SU];
+#pragma unroll
+        for (int k = 0; k < SU; ++k) {
+            const int e = e0 + k * NT;
+            const int lr = e / WS4, cc = e - lr * WS4 - PADL / 4;
+            const int yy = yb0 - hg + lr;
+            v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (e < n4 && yy >= 0 && yy < H && cc >= 0 && cc < W4)
+                v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        }
+#pragma unroll
+        for (int k = 0; k < SU; ++k)
+            if (e0 + k * NT < n4) xs4[e0 + k * NT] = v[k];
     }
     __syncthreads();
 
@@ -329,13 +344,12 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     const int nbx = W / TRX, nby = (yb1 - yb0 + TRY - 1) / TRY;
     float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
-        const tmr_unit_t &un = a.units[u];
+        const tmr_unit_t &un = units[u];  // restrict: scalar loads, no wait behind the stores
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
         const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
         const int Ho = H - h + 1, Wo = W - w + 1;
-        const float sc = a.squeeze ? 1.0f : *a.scale;
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;  // correctly rounded reciprocal
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
@@ -469,7 +483,7 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     TMR_REQUIRE(C < 65536 && B < 65536);
     dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
     if (rows)
-        hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
+        hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
     else
         hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
     TMR_CHECK_LAUNCH();

@@ -134,6 +134,37 @@ def test_xcorr_large_vs_oracle(k):
         assert normwise(got[b], ref) <= TOL
 
 
+@pytest.mark.parametrize("H,W", [(29, 37), (40, 30), (33, 64), (70, 128)])
+def test_xcorr_units_both_kernels_vs_oracle(H, W):
+    """Several units per image with mixed (rectangular) template sizes through
+    TMREngine.match: W % 4 == 0 runs xcorr_rows_kernel (lane tiles over the
+    whole band, border computed in-tile), other widths the generic
+    xcorr_kernel; band edges (H not a multiple of the 32-row band) included."""
+    C = 24
+    P = {k: v.to(DEV) for k, v in synth.reference_state_dict(0, cin=16, emb=C).items()}
+    eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C))
+    fp = synth.normal(77 + W, (2, C, H, W))
+    shapes = [(3, 3), (7, 5), (13, 9), (1, 1), (5, 11), (9, 3)]
+    boxes, ui = [], []
+    for u, (kh, kw) in enumerate(shapes):
+        kh, kw = min(kh, H // 2 * 2 - 1), min(kw, W // 2 * 2 - 1)
+        boxes.append(synth.exemplar_box(kh, H, W, (5 * u) % (H - kh), (7 * u) % (W - kw), kw))
+        ui.append(u // 3)
+    boxes = np.stack(boxes)
+    got, _ = eng.match(cuda(fp), ui, boxes)
+    got = got.cpu().numpy()
+    for u in range(len(ui)):
+        roi, ht, wt = oracle.template_size(boxes[u], H, W)
+        t = oracle.roi_align(fp[ui[u]], roi, ht, wt)
+        ref = oracle.xcorr(fp[ui[u]], t, 1.0)
+        assert normwise(got[u], ref) <= TOL, (u, ht, wt, normwise(got[u], ref))
+        ph, pw = ht // 2, wt // 2
+        if ph:
+            assert (got[u][:, :ph] == 0).all() and (got[u][:, H - ph:] == 0).all()
+        if pw:
+            assert (got[u][:, :, :pw] == 0).all() and (got[u][:, :, W - pw:] == 0).all()
+
+
 # ----------------------------------------------------------------- convs
 @pytest.mark.parametrize("C,N,H,W,ks", [(64, 64, 32, 40, 3), (40, 72, 17, 33, 3), (16, 16, 24, 24, 5),
                                         (24, 8, 20, 20, 1), (1024, 1024, 16, 32, 3), (12, 12, 9, 9, 7)])
