@@ -265,11 +265,12 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
 // specialisation: reads are aligned b128, pairs are picked at compile time.
 constexpr int PADL = 20;  // >= 15 + 3 (max half-width + OFF), multiple of 4
 constexpr int PADR = 24;  // covers the window over-read past column W
-constexpr int TRY = 4, TRX = 4;
+constexpr int TRY = 4;  // max tile rows (the LDS slack rows cover it)
 
-template <int KW>
+template <int KW, int TRY, int TRX>
 __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, int lcol0,
-                                          const float *__restrict__ tc, int h, f32x2 (&pa)[TRY][2]) {
+                                          const float *__restrict__ tc, int h,
+                                          f32x2 (&pa)[TRY][TRX / 2]) {
     constexpr int OFF = (4 - ((KW / 2) & 3)) & 3;
     constexpr int NV = (OFF + KW + TRX + 3) / 4;   // b128 reads per row (+1 float for odd pairs)
     constexpr int NO = (OFF + KW + TRX - 2) / 2;   // odd pairs (x[2m+1], x[2m+2])
@@ -299,6 +300,57 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
                     const f32x2 xv2 = (s0 & 1) ? xo[s0 >> 1] : xe[s0 >> 1];
                     pa[r][q] = __builtin_elementwise_fma(xv2, tt, pa[r][q]);
                 }
+            }
+        }
+    }
+}
+
+// One unit's band for the rows kernel in TY x TX lane tiles.
+template <int TY, int TX>
+__device__ __forceinline__ void rows_unit(const float *xs, int WS, int W, int yb0, int yb1, int hg, int h,
+                                          int w, int ph, int pw, int Ho, int Wo,
+                                          const float *__restrict__ tc, float denom, float rden, float sc,
+                                          float *op, float *rp, float &vmax) {
+    const int nbx = W / TX, nby = (yb1 - yb0 + TY - 1) / TY;
+    for (int task = threadIdx.x; task < nbx * nby; task += NT) {
+        const int c0 = (task % nbx) * TX, y0 = yb0 + (task / nbx) * TY;
+        f32x2 pa[TY][TX / 2];
+#pragma unroll
+        for (int r = 0; r < TY; ++r)
+#pragma unroll
+            for (int q = 0; q < TX / 2; ++q) pa[r][q] = f32x2{0.0f, 0.0f};
+        const int lrow0 = y0 - yb0 + hg - ph;
+        const int lcol0 = PADL + c0 - pw - ((4 - (pw & 3)) & 3);
+        // tiles wholly in the border rows or columns only store zeros
+        const bool live = y0 + TY > ph && y0 < ph + Ho && c0 + TX > pw && c0 < pw + Wo;
+        if (live) switch (w) {
+#define TMR_W(K) case K: corr_tile<K, TY, TX>(xs, WS, lrow0, lcol0, tc, h, pa); break;
+            TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
+            TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
+#undef TMR_W
+            default: break;  // even widths never reach this kernel (template sizes are odd)
+        }
+#pragma unroll
+        for (int r = 0; r < TY; ++r) {
+            const int y = y0 + r;
+            if (y >= yb1) break;
+            const bool vy = y >= ph && y < ph + Ho;
+            float v[TX];
+#pragma unroll
+            for (int q = 0; q < TX; ++q) {
+                const int cx = c0 + q;
+                const float acc = (q & 1) ? pa[r][q >> 1].y : pa[r][q >> 1].x;
+                v[q] = (vy && cx >= pw && cx < pw + Wo) ? div_cr(acc, denom, rden) * sc : 0.0f;
+                vmax = fmaxf(vmax, fabsf(v[q]));
+            }
+            const size_t o = (size_t)y * W + c0;
+#pragma unroll
+            for (int q = 0; q < TX; q += 4) {
+                *reinterpret_cast<float4 *>(op + o + q) = float4{v[q], v[q + 1], v[q + 2], v[q + 3]};
+                if (rp)
+                    *reinterpret_cast<float4 *>(rp + o + q) =
+                        float4{fmaxf(v[q], 0.0f), fmaxf(v[q + 1], 0.0f), fmaxf(v[q + 2], 0.0f),
+                               fmaxf(v[q + 3], 0.0f)};
             }
         }
     }
@@ -341,7 +393,6 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     __syncthreads();
 
     const size_t plane = (size_t)H * W;
-    const int nbx = W / TRX, nby = (yb1 - yb0 + TRY - 1) / TRY;
     float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
         const tmr_unit_t &un = units[u];  // restrict: scalar loads, no wait behind the stores
@@ -356,42 +407,10 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
                               : outp + ((size_t)u * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
-        for (int task = threadIdx.x; task < nbx * nby; task += NT) {
-            const int c0 = (task % nbx) * TRX, y0 = yb0 + (task / nbx) * TRY;
-            f32x2 pa[TRY][2];
-#pragma unroll
-            for (int r = 0; r < TRY; ++r) pa[r][0] = pa[r][1] = f32x2{0.0f, 0.0f};
-            const int lrow0 = y0 - yb0 + hg - ph;
-            const int lcol0 = PADL + c0 - pw - ((4 - (pw & 3)) & 3);
-            // tiles wholly in the border rows or columns only store zeros
-            const bool live = y0 + TRY > ph && y0 < ph + Ho && c0 + TRX > pw && c0 < pw + Wo;
-            if (live) switch (w) {
-#define TMR_W(K) case K: corr_tile<K>(xs, WS, lrow0, lcol0, tc, h, pa); break;
-                TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
-                TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
-#undef TMR_W
-                default: break;  // even widths never reach this kernel (host check)
-            }
-#pragma unroll
-            for (int r = 0; r < TRY; ++r) {
-                const int y = y0 + r;
-                if (y >= yb1) break;
-                const bool vy = y >= ph && y < ph + Ho;
-                float v[TRX];
-#pragma unroll
-                for (int q = 0; q < TRX; ++q) {
-                    const int cx = c0 + q;
-                    const float acc = (q & 1) ? pa[r][q >> 1].y : pa[r][q >> 1].x;
-                    v[q] = (vy && cx >= pw && cx < pw + Wo) ? div_cr(acc, denom, rden) * sc : 0.0f;
-                    vmax = fmaxf(vmax, fabsf(v[q]));
-                }
-                const size_t o = (size_t)y * W + c0;
-                *reinterpret_cast<float4 *>(op + o) = float4{v[0], v[1], v[2], v[3]};
-                if (rp)
-                    *reinterpret_cast<float4 *>(rp + o) =
-                        float4{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f), fmaxf(v[2], 0.0f), fmaxf(v[3], 0.0f)};
-            }
-        }
+        // 4x4 tiles: one 16-B store per lane row (1 KB per wave row).  2x8
+        // tiles (twice the FMAs per scalar tap-row load) measured 5.1 vs 5.5
+        // ms at k = 9 but 10.4 vs 7.4 at k = 11 and 16.4 vs 11.4 at k = 15.
+        rows_unit<4, 4>(xs, WS, W, yb0, yb1, hg, h, w, ph, pw, Ho, Wo, tc, denom, rden, sc, op, rp, vmax);
     }
     if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
         for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
