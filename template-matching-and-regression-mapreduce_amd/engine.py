@@ -224,8 +224,23 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool, packe
     return out
 
 
+def _h2d(arr: np.ndarray, device, dtype=None) -> torch.Tensor:
+    """A small host array on the device WITHOUT a stream sync: staged through
+    torch's caching pinned-memory allocator and copied non_blocking (the
+    allocator keeps the pinned block until the copy's stream event has
+    completed).  A pageable `.to(device)` synchronises the stream, leaving the
+    GPU idle while the host prepares the next launches."""
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if dtype is not None:
+        t = t.to(dtype)
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def _units_to_device(units: np.ndarray, device) -> torch.Tensor:
-    return torch.from_numpy(units.view(np.uint8).copy()).to(device, non_blocking=False)
+    return _h2d(units.view(np.uint8), device)
 
 
 class TMREngine:
@@ -441,7 +456,7 @@ class TMREngine:
         dev = fp.device
         units_d = _units_to_device(units, dev)
         img_units = host.image_ranges(unit_image, B)  # units are sorted by image
-        img_units_d = torch.as_tensor(img_units, device=dev)
+        img_units_d = _h2d(np.asarray(img_units), dev)
         tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
         call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
         Co = 1 if cfg.squeeze else C
@@ -466,7 +481,7 @@ class TMREngine:
         U, C1, H, W = f_tm.shape
         dev = f_tm.device
         C0 = fp.shape[1] if cfg.fusion else 0
-        ui = torch.as_tensor(np.asarray(unit_image, np.int32), device=dev)
+        ui = _h2d(np.asarray(unit_image, np.int32), dev)
         src0 = fp if cfg.fusion else None
         if cfg.decoder_num_layer == 1:
             B = fp.shape[0]
@@ -597,7 +612,7 @@ class TMREngine:
         unit_image = [int(i) for i in unit_image]
         fp, f0 = self.project(feats, want_f0=want_aux)
         if self.cfg.no_matcher:
-            ui = torch.as_tensor(unit_image, device=fp.device, dtype=torch.long)
+            ui = _h2d(np.asarray(unit_image, np.int64), fp.device)
             f_tm = fp.index_select(0, ui).contiguous()
             relu = torch.relu(f_tm) if want_aux else None
         else:
@@ -617,7 +632,7 @@ class TMREngine:
         H, W = o.shape[-2:]
         dev = o.device
         cap = H * W
-        prm = torch.from_numpy(params.view(np.uint8).copy()).to(dev)
+        prm = _h2d(params.view(np.uint8), dev)
         prob = torch.empty((U, H, W), device=dev, dtype=torch.float32)
         logits = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         box = torch.empty((U * cap, 4), device=dev, dtype=torch.float32)
@@ -641,9 +656,9 @@ class TMREngine:
         T = int(cand_off[-1])
         work = torch.empty(max(load().tmr_nms_work_size(T, int(mask_off[-1])), 1), device=dev,
                            dtype=torch.uint8)
-        seg_d = torch.as_tensor(np.asarray(seg_units, np.int32), device=dev)
-        coff_d = torch.as_tensor(cand_off, device=dev)
-        moff_d = torch.as_tensor(mask_off, device=dev)
+        seg_d = _h2d(np.asarray(seg_units, np.int32), dev)
+        coff_d = _h2d(np.asarray(cand_off), dev)
+        moff_d = _h2d(np.asarray(mask_off), dev)
         out_l = torch.empty((T, 2), device=dev, dtype=torch.float32)
         out_b = torch.empty((T, 4), device=dev, dtype=torch.float32)
         out_r = torch.empty((T, 2), device=dev, dtype=torch.float32)
