@@ -179,13 +179,25 @@ __global__ __launch_bounds__(64) void reduce_kernel(const int64_t *__restrict__ 
             if (out_keep) out_keep[dst] = li;
         }
         cnt += __popcll(kept);
+        // OR the kept rows' words into the later blocks: lane k gathers
+        // column block k (coalesced across lanes); the kept rows (a
+        // wave-uniform set) are walked 8 at a time so 8 independent loads are
+        // in flight per wait instead of one load latency per kept row
         for (int k = ib + 1 + lane; k < nb; k += 64) {
             uint64_t acc = 0;
             uint64_t kb = kept;
             while (kb) {
-                const int b = __builtin_ctzll(kb);
-                kb &= kb - 1;
-                acc |= mask[(int64_t)(ib * 64 + b) * nb + k];
+                uint64_t v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    v[t] = 0;
+                    if (kb) {
+                        const int b = __builtin_ctzll(kb);
+                        kb &= kb - 1;
+                        v[t] = mask[(int64_t)(ib * 64 + b) * nb + k];
+                    }
+                }
+                acc |= ((v[0] | v[1]) | (v[2] | v[3])) | ((v[4] | v[5]) | (v[6] | v[7]));
             }
             removed[k] |= acc;
         }
