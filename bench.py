@@ -131,8 +131,15 @@ def main():
     a = ap.parse_args()
 
     rank, world, local = driver.dist_env()
+    # one process per GPU; a rehearsal with more ranks than GPUs (gloo on a
+    # 1-GPU box) wraps the local rank onto the visible devices
+    local = local % max(1, torch.cuda.device_count())
+    backend = os.environ.get("TMR_BENCH_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
