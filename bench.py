@@ -40,6 +40,7 @@ METRIC = "images/sec (whole node) match+regress+NMS; % HBM/MFMA roofline at 1/2/
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), spec
 # dense fp16/bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (MI355X_MICROARCH.md, ~2.5 PF)
 F16_PEAK_TFLOPS = 2516.6
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 # 16-bit MFMA terms per product of the split decoder kernel (conv_split.hip)
 SPLIT_TERMS = {"fp32": 3, "bf16": 1, "f16": 1}
 EMB, CIN, KS = 512, 256, 3
@@ -169,6 +170,7 @@ def main():
     if world > 1:
         dist.barrier()
     eng.decoder_events = []
+    eng.xcorr_events = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -182,7 +184,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     dec_ms = [s.elapsed_time(e) for s, e in eng.decoder_events]
-    eng.decoder_events = None
+    xc_ms = [s.elapsed_time(e) for s, e in eng.xcorr_events]
+    eng.decoder_events = eng.xcorr_events = None
     kept = [int(x.shape[0]) for x in last]
 
     if rank == 0:
@@ -238,6 +241,19 @@ def main():
                          "path_algorithmic_tflop_per_step": round(
                              decoder_flops_per_unit() * B * E / 1e12, 2)},
         }
+        # the correlation kernel (SURVEY.md 8d "kernel 2"): HBM-bound for small
+        # templates, VALU-bound for k >= 11; both fractions, algorithmic work
+        xs = float(np.mean(xc_ms)) / 1e3
+        out["roofline_xcorr"] = {
+            "kernel": "tmr_xcorr (xcorr_rows_kernel: depthwise xcorr + /hw + pad + scale + max|f_TM|)",
+            "bound": "hbm" if cfg["kmax"] <= 9 else "valu",
+            "avg_launch_ms": round(1e3 * xs, 3),
+            "hbm_achieved": round(eng.last_xcorr_bytes / xs / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
+            "hbm_unit": "GB/s", "hbm_frac": round(eng.last_xcorr_bytes / xs / 1e9 / HBM_PEAK_GBS, 4),
+            "valu_achieved": round(eng.last_xcorr_flops / xs / 1e12, 2), "valu_peak": FP32_PEAK_TFLOPS,
+            "valu_unit": "TFLOP/s", "valu_frac": round(eng.last_xcorr_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "basis": "per unit: read + write C*H*W fp32 (the fp plane read once per unit, f_TM written), "
+                     "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)"}
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds, cfg["cls"], cfg["iou"])
         else:

@@ -253,6 +253,9 @@ class TMREngine:
         # when a list, decode() appends (start, end) torch.cuda.Events recorded
         # on the launch stream around the fused decoder kernel (bench.py)
         self.decoder_events = None
+        self.xcorr_events = None
+        self.last_xcorr_flops = 0.0
+        self.last_xcorr_bytes = 0.0
         # conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM): compute conv_fp once
         # per image when several exemplars share it (fp32, changes only the
         # summation order; same 1e-5 contract)
@@ -466,10 +469,22 @@ class TMREngine:
         scale = self.P["matcher.scale"].detach().float().contiguous()
         # max |f_TM| fused in the kernel: per-workgroup maxima into 256 slots
         slots = torch.zeros(ABSMAX_SLOTS, device=dev, dtype=torch.float32)
+        ev = None
+        if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh, mw,
              ptr(scale),
              int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
              ptr(work) if work is not None else None, ptr(slots), stream())
+        if ev is not None:
+            ev[1].record()
+            self.xcorr_events.append(ev)
+        # SURVEY.md 8d algorithmic work of the launch: per unit 2*C*(H-h+1)(W-w+1)*h*w
+        # FLOPs, read + write C*H*W fp32
+        ht, wt = units["ht"].astype(np.float64), units["wt"].astype(np.float64)
+        self.last_xcorr_flops = float(np.sum(2.0 * C * (H - ht + 1) * (W - wt + 1) * ht * wt))
+        self.last_xcorr_bytes = 2.0 * 4 * C * H * W * U
         self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 
