@@ -375,12 +375,17 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     constexpr int SU = 8;
     const int W4 = W / 4, WS4 = WS / 4, n4 = a.LR * WS4;
     float4 *xs4 = reinterpret_cast<float4 *>(xs);
+    // e / WS4 as one fp32 multiply: exact for e < 2^16 (the quotient's
+    // rounding error is < 2^-8 of the 0.5 / WS4 margin); the integer
+    // division by a runtime divisor cost ~30 VALU per staged float4, which
+    // dominated the instruction count at small templates (PMC: 7x the FMAs)
+    const float rws4 = 1.0f / (float)WS4;
     for (int e0 = threadIdx.x; e0 < n4; e0 += NT * SU) {
         float4 v[SU];
 #pragma unroll
         for (int k = 0; k < SU; ++k) {
             const int e = e0 + k * NT;
-            const int lr = e / WS4, cc = e - lr * WS4 - PADL / 4;
+            const int lr = (int)(((float)e + 0.5f) * rws4), cc = e - lr * WS4 - PADL / 4;
             const int yy = yb0 - hg + lr;
             v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
             if (e < n4 && yy >= 0 && yy < H && cc >= 0 && cc < W4)
