@@ -63,6 +63,12 @@ constexpr int TW = 32;       // output cols per block
 // waves per block: 8 (2 along n x 4 along rows, 128 accumulator VGPRs, two
 // waves per SIMD) or 4 (1 x 4, 256 accumulators, one wave per SIMD: half
 // the LDS fragment reads per MFMA)
+#ifndef TMR_SPLIT_PXG  // XCD block groups: pixel tiles x channel tiles
+#define TMR_SPLIT_PXG 8
+#endif
+#ifndef TMR_SPLIT_NG
+#define TMR_SPLIT_NG 4
+#endif
 #ifndef TMR_SPLIT_NW
 #define TMR_SPLIT_NW 8
 #endif
@@ -255,7 +261,8 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
     int nt, mt, u;
     {
-        constexpr int PXG = 8, NG = 4;  // one XCD wave of 32 blocks = 8 pixel tiles x 4 channel tiles
+        // one XCD wave of 32 blocks = PXG pixel tiles x NG channel tiles
+        constexpr int PXG = TMR_SPLIT_PXG, NG = TMR_SPLIT_NG;
         const int per_unit = a.NT * a.MT;
         u = L / per_unit;
         const int r = L - u * per_unit;
