@@ -69,6 +69,9 @@ constexpr int TW = 32;       // output cols per block
 #ifndef TMR_SPLIT_NG
 #define TMR_SPLIT_NG 4
 #endif
+#ifndef TMR_SPLIT_ACC_NT  // non-temporal stores of the tiled acc0 (read back by a later launch; +0.4% config B)
+#define TMR_SPLIT_ACC_NT 1
+#endif
 #ifndef TMR_SPLIT_NW
 #define TMR_SPLIT_NW 8
 #endif
@@ -529,7 +532,12 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
         for (int in = 0; in < NIN; ++in)
 #pragma unroll
-            for (int jp = 0; jp < 8; ++jp) o[(in * 8 + jp) * 64] = acc[in][jp] * inv;
+            for (int jp = 0; jp < 8; ++jp) {
+                if (TMR_SPLIT_ACC_NT)
+                    __builtin_nontemporal_store(acc[in][jp] * inv, o + (in * 8 + jp) * 64);
+                else
+                    o[(in * 8 + jp) * 64] = acc[in][jp] * inv;
+            }
         return;
     }
     // the block's bias and head weights through LDS (the main loop's last
