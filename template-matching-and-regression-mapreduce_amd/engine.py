@@ -65,18 +65,20 @@ def _version_key(ts: Sequence[torch.Tensor]):
 
 
 class _PackCache:
-    """Derived weight layouts keyed on the parameters' storage and version."""
+    """Derived weight layouts keyed on the parameters' storage and version AND
+    on the tensor objects themselves (weak references): a rebuilt tensor that
+    reuses a freed address at _version 0 never hits a stale entry."""
 
     def __init__(self):
-        self._d: Dict[str, Tuple[tuple, object]] = {}
+        self._d: Dict[str, Tuple[tuple, tuple, object]] = {}
 
     def get(self, name: str, tensors: Sequence[torch.Tensor], build):
         key = _version_key(tensors)
         hit = self._d.get(name)
-        if hit is not None and hit[0] == key:
-            return hit[1]
+        if hit is not None and hit[0] == key and all(r() is t for r, t in zip(hit[1], tensors)):
+            return hit[2]
         val = build()
-        self._d[name] = (key, val)
+        self._d[name] = (key, tuple(weakref.ref(t) for t in tensors), val)
         return val
 
 
@@ -529,10 +531,18 @@ class TMREngine:
                 xmax0 = self._feat_absmax(feats)
                 tm_max = self._memo_absmax(f_tm, "ftm", lambda: absmax(f_tm))
                 if share:
+                    # the fp half is its own launch (tmr_split_conv_store) with
+                    # its own activation scale
                     xmax1 = tm_max
+                    xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0,
+                                        ones=False)
                 else:
+                    # ONE launch reads both sources and undoes ONE activation
+                    # scale (conv_split.hip takes one xmax per launch): both
+                    # record sets are packed with max(max|f_TM|, xmax0)
                     xmax1 = absmax(tm_max, xmax0.clone())
-                xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0, ones=False)
+                    xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax1,
+                                        ones=False)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
             elif splitk:

@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from .backbone import build_backbone
 from .engine import PathConfig, TMREngine
 from .regression_head import BboxesHead, Decoder_model, ObjectnessHead
 from .template_matching import TemplateMatching, _box_host
@@ -94,11 +95,12 @@ class matching_net(nn.Module):
 
 
 def build_model(args, backbone=None):
-    """models/__init__.py:4-10.  The reference builds the SAM backbone from
-    ``args``; that backbone is outside the accelerated path, so the caller
-    hands it in (any nn.Module with ``num_channels``)."""
+    """models/__init__.py:4-10: ``build_model(args)`` with the reference's
+    signature; the backbone comes from ``build_backbone(args)`` (the registry
+    in backbone.py: the frozen encoder stays on stock PyTorch-ROCm).  The
+    optional ``backbone`` module (extension) bypasses the registry."""
     if backbone is None:
-        raise ValueError("pass the (frozen) backbone module: it stays on stock PyTorch-ROCm")
+        backbone = build_backbone(args)
     if args.modeltype == "matching_net":
         return matching_net(backbone, args)
     raise KeyError(args.modeltype)

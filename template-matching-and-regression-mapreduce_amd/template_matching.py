@@ -1,8 +1,14 @@
 """Drop-in ``TemplateMatching`` (reference: models/template_matching.py:8-99).
 
-Same constructor, parameters (``scale``), state_dict keys and forward
-signature; the template extraction (RoIAlign / prototype) and the depthwise
-cross-correlation run in libtmr.so (tmr_templates, tmr_xcorr).
+Same constructor, parameters (``scale``), state_dict keys, public members
+(``extract_function``, ``matching_algorithm``, ``cross_correlation``,
+``extract_template``, ``extract_prototype``, ``matcher``) and forward
+signature.  ``matcher`` returns the UNSCALED map and ``forward`` applies
+``* self.scale`` (:95-99), so ``model.matcher(f, ex) * model.matcher.scale``
+is what the reference computes.  The template extraction (RoIAlign /
+prototype) and the depthwise cross-correlation run in libtmr.so
+(tmr_templates, tmr_xcorr); the scale is applied in the correlation kernel's
+epilogue (one rounding of the product, as ``f * self.scale``).
 """
 from __future__ import annotations
 
@@ -11,8 +17,8 @@ import torch
 from torch import nn
 
 from . import host
-from ._lib import require_gpu
-from .engine import PathConfig, TMREngine
+from ._lib import UNIT_DTYPE, TMRError, call, ptr, require_gpu, stream
+from .engine import PathConfig, TMREngine, _h2d, _units_to_device
 
 
 def _box_host(exemplar_coord) -> np.ndarray:
@@ -24,28 +30,36 @@ def _box_host(exemplar_coord) -> np.ndarray:
 class TemplateMatching(nn.Module):
     def __init__(self, template_type, squeeze=False):
         super().__init__()
-        if template_type not in host.TEMPLATE_TYPES:
-            raise KeyError(template_type)  # template_types[...] lookup, :16-20
-        self.template_type = template_type
         self.squeeze = squeeze
         self.scale = nn.Parameter(torch.tensor([1.0], dtype=torch.float32))
         self.avg_pool = nn.AdaptiveAvgPool2d((1, 1))  # parameter-free, kept for parity
+        template_types = {
+            "roi_align": self.extract_template,
+            "prototype": self.extract_prototype,
+        }
+        self.extract_function = template_types[template_type]  # KeyError like :16-20
+        self.template_type = template_type
+        self.matching_algorithm = self.cross_correlation
 
-    def _engine(self, C: int) -> TMREngine:
-        cfg = PathConfig(emb_dim=C, squeeze=self.squeeze, template_type=self.template_type)
-        return TMREngine({"matcher.scale": self.scale}, cfg)
-
-    def matcher(self, sample, exemplars):
-        """Per-image template + xcorr (:79-93); returns the *scaled* map."""
-        require_gpu(sample, "feature")
-        B, C, H, W = sample.shape
-        boxes = np.stack([_box_host(exemplars[b][0]) for b in range(B)])
-        out, _ = self._engine(C).match(sample.float().contiguous(), list(range(B)), boxes)
-        return out
-
-    def forward(self, feature, exemplars):
-        # the kernel applies `* self.scale` (:97) in its epilogue
-        return self.matcher(feature, exemplars)
+    # ---------------------------------------------------------------- pieces
+    def cross_correlation(self, feature, template):
+        """:23-41: depthwise conv2d(feature, template, groups) / (h*w) + zero pad
+        back to the feature size (summed over channels when squeeze).  feature
+        [bs,c,H,W], template [bs,c,h,w] (h, w odd) -> [1, bs*c | 1, H, W]."""
+        require_gpu(feature, "feature")
+        require_gpu(template, "template")
+        bs, c, h, w = template.shape
+        if feature.shape[:2] != template.shape[:2]:
+            raise TMRError(f"feature {tuple(feature.shape)} and template {tuple(template.shape)} "
+                           "must agree in (batch, channels)")
+        if h % 2 == 0 or w % 2 == 0:
+            raise TMRError("cross_correlation: odd template sizes only (extract_template makes "
+                           "them odd, template_matching.py:72-73)")
+        if self.squeeze and bs != 1:
+            raise TMRError("cross_correlation: squeeze sums over bs*c channels; bs must be 1")
+        one = torch.ones(1, device=feature.device, dtype=torch.float32)
+        return _xcorr(feature, template, one, self.squeeze).reshape(
+            1, 1 if self.squeeze else bs * c, *feature.shape[-2:])
 
     def extract_template(self, f, exemplar_coord):
         """roi_align template [1,C,Ht,Wt] (:55-76)."""
@@ -56,9 +70,6 @@ class TemplateMatching(nn.Module):
         return self._templates(f, exemplar_coord, "prototype")
 
     def _templates(self, f, exemplar_coord, ttype):
-        from ._lib import call, ptr, stream
-        from .engine import _units_to_device
-
         require_gpu(f, "feature")
         f = f.float().contiguous()
         _, C, H, W = f.shape
@@ -67,3 +78,69 @@ class TemplateMatching(nn.Module):
         ud = _units_to_device(units, f.device)
         call("tmr_templates", ptr(f), 1, C, H, W, ptr(ud), 1, mh, mw, ptr(t), stream())
         return t.view(1, C, int(units["ht"][0]), int(units["wt"][0]))
+
+    # ---------------------------------------------------------------- matcher
+    def _native(self) -> bool:
+        """True while extract_function / matching_algorithm are this module's
+        own (then the whole per-image loop is one batched launch)."""
+        ef, ma = self.extract_function, self.matching_algorithm
+        own_ef = getattr(ef, "__self__", None) is self and getattr(ef, "__func__", None) in (
+            TemplateMatching.extract_template, TemplateMatching.extract_prototype)
+        own_ma = getattr(ma, "__self__", None) is self and \
+            getattr(ma, "__func__", None) is TemplateMatching.cross_correlation
+        return own_ef and own_ma
+
+    def _match(self, sample, exemplars, scale: torch.Tensor):
+        require_gpu(sample, "feature")
+        B, C, H, W = sample.shape
+        if not self._native():
+            # a caller replaced a member: follow the reference's loop (:79-93)
+            maps = []
+            for b in range(B):
+                now_f = sample[b].unsqueeze(0)
+                t = self.extract_function(now_f, exemplars[b][0])
+                maps.append(self.matching_algorithm(now_f, t))
+            f = torch.concat(maps, dim=0)
+            return f * scale if scale is not None else f
+        ttype = "roi_align" if self.extract_function.__func__ is TemplateMatching.extract_template \
+            else "prototype"
+        boxes = np.stack([_box_host(exemplars[b][0]) for b in range(B)])
+        cfg = PathConfig(emb_dim=C, squeeze=self.squeeze, template_type=ttype)
+        if scale is None:
+            scale = torch.ones(1, device=sample.device, dtype=torch.float32)
+        eng = TMREngine({"matcher.scale": scale}, cfg)
+        out, _ = eng.match(sample.float().contiguous(), list(range(B)), boxes)
+        return out
+
+    def matcher(self, sample, exemplars):
+        """Per-image template + xcorr (:79-93); the UNSCALED map, like the reference."""
+        return self._match(sample, exemplars, None)
+
+    def forward(self, feature, exemplars):
+        """:95-99: matcher(...) * scale, the product taken in the kernel epilogue."""
+        return self._match(feature, exemplars, self.scale)
+
+
+def _xcorr(feature: torch.Tensor, template: torch.Tensor, scale: torch.Tensor,
+           squeeze: bool) -> torch.Tensor:
+    """tmr_xcorr with caller-provided templates: unit b correlates feature[b]
+    with template[b] -> [bs, C|1, H, W] (the pad border exactly zero)."""
+    feature = feature.float().contiguous()
+    template = template.float().contiguous()
+    bs, C, H, W = feature.shape
+    _, _, h, w = template.shape
+    if h > H or w > W:
+        raise TMRError(f"template {h}x{w} larger than the {H}x{W} feature map")
+    units = np.zeros(bs, UNIT_DTYPE)
+    units["image"] = np.arange(bs)
+    units["ht"], units["wt"] = h, w
+    units["tmpl_offset"] = np.arange(bs) * (C * h * w)
+    dev = feature.device
+    ud = _units_to_device(units, dev)
+    iu = _h2d(np.arange(bs + 1, dtype=np.int32), dev)
+    out = torch.empty((bs, 1 if squeeze else C, H, W), device=dev, dtype=torch.float32)
+    work = torch.empty((bs, C, H, W), device=dev, dtype=torch.float32) if squeeze else None
+    call("tmr_xcorr", ptr(feature), bs, C, H, W, ptr(template), ptr(ud), ptr(iu), bs, h, w,
+         ptr(scale.detach().float().contiguous()), int(squeeze), ptr(out), None,
+         ptr(work) if work is not None else None, None, stream())
+    return out

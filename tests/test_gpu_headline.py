@@ -1,0 +1,264 @@
+"""GPU parity at the graded workloads and in the reference's own call forms.
+
+* config B exactly as bench.py runs it (64 images x 3 exemplars, the same
+  seeds, weights and TMREngine.detect call): images 0, 31 and 63 (9 units, the
+  first / middle / last of the batch's per-image offsets, tiled acc0 slabs and
+  record packs) against the torch-CPU oracle;
+* config E (192^2 maps, 16 exemplars, templates up to 31x31) as bench.py runs
+  it, the last image of the batch;
+* the unshared folded decoder path (E = 1) with |f_TM| far above |features|;
+* the module API driven in the exact call forms of demo.py:106-130 and
+  trainer.py:75-150.
+
+Tolerances: fp32 maps normwise <= 1e-5; peaks / keep lists /
+counts bit-exact given the GPU's own maps; the end-to-end agreement with the
+oracle's maps is reported (oracle/agreement.py) and held to its contract.
+"""
+import json
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import agreement
+import oracle
+import tmr_amd
+from tmr_amd import host, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+DEV = torch.device("cuda:0")
+
+
+def normwise(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)) if a.size else 0.0
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def cuda(x):
+    return torch.as_tensor(x).to(DEV)
+
+
+def _oracle_detect_on_maps(prob, reg, boxes, thr, iou):
+    """The reference caller sequence (demo.py:111-130) on given maps."""
+    ls, bs, rs = [], [], []
+    for u in range(len(prob)):
+        l_, b_, r_ = oracle.get_pred_boxes_prob([prob[u]], [reg[u]], [boxes[u][None]], thr)
+        ls.append(l_[0]); bs.append(b_[0]); rs.append(r_[0])
+    L, B, R = oracle.nms_lists([np.concatenate(ls)], [np.concatenate(bs)], [np.concatenate(rs)], iou)
+    return L[0], B[0], R[0]
+
+
+def _check_images(P, feats, ex, images, thr, iou, hf):
+    """bench-batch run through TMREngine.detect + forward_units; per checked
+    image: maps vs the oracle forward, detect() vs the oracle's peaks+NMS on
+    the GPU's maps (bit-exact), agreement with the oracle's own maps."""
+    B, E = ex.shape[:2]
+    Pd = {k: v.to(DEV) for k, v in P.items()}
+    eng = tmr_amd.TMREngine(Pd, tmr_amd.PathConfig())
+    fd = cuda(feats)
+    L, Bx, R = eng.detect(fd, ex, cls_ths=thr, iou_threshold=iou)  # the bench step
+    ui = np.repeat(np.arange(B), E)
+    r = eng.forward_units(fd, ui, ex.reshape(-1, 4))
+    o, b = r["o"].cpu().numpy(), r["b"].cpu().numpy()
+    lines = []
+    for img in images:
+        units = [img * E + e for e in range(E)]
+        omaps = []
+        for e, u in enumerate(units):
+            ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[img:img + 1]),
+                                                [torch.from_numpy(ex[img, e:e + 1])], P)
+            ro, rb = ro[0][0].numpy(), rb[0][0].numpy()
+            assert normwise(o[u], ro) <= TOL, (img, e, normwise(o[u], ro))
+            assert normwise(b[u], rb) <= TOL, (img, e, normwise(b[u], rb))
+            omaps.append((oracle.sigmoid_cr(ro[0]), rb))
+        gmaps = agreement.unit_maps(o[units], b[units])
+        gl, gb, gr = _oracle_detect_on_maps([m[0] for m in gmaps], [m[1] for m in gmaps],
+                                            list(ex[img]), thr, iou)
+        assert bits_equal(L[img].cpu().numpy(), gl), img
+        assert bits_equal(Bx[img].cpu().numpy(), gb), img
+        assert bits_equal(R[img].cpu().numpy(), gr), img
+        rep = agreement.compare(omaps, gmaps, list(ex[img]), thr, iou)
+        agreement.check(rep)
+        lines.append(agreement.report_line(f"image {img} oracle-maps vs GPU-maps:", rep))
+    print("\n".join(lines))
+    return [int(x.shape[0]) for x in L]
+
+
+def test_headline_batch_config_b():
+    """bench.py config B, bit for bit the same inputs (seeds 1000 / 2000)."""
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, 64, 256, 64, 64)
+    ex, _ = synth.exemplar_set(2000, 64, 3, 128, 128, 3, 15)
+    kept = _check_images(P, feats, ex, (0, 31, 63), 0.1, 0.5, 64)
+    print("config B mean kept per image:", float(np.mean(kept)))
+
+
+def test_config_e_last_image():
+    """bench.py config E (8 x 192^2, E = 16, k 3..31): the batch's last image."""
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, 8, 256, 96, 96)
+    ex, ks = synth.exemplar_set(2000, 8, 16, 192, 192, 3, 31)
+    assert ks[7].max() >= 25  # the large templates are in the checked image
+    _check_images(P, feats, ex, (7,), 0.1, 0.5, 96)
+
+
+@pytest.mark.parametrize("scale", [64.0, 1000.0])
+def test_unshared_folded_path_large_ftm(scale):
+    """E = 1 (U < 2B): one split-conv launch reads the folded fp-half records and
+    the f_TM records under ONE activation scale; |f_TM| (matcher.scale) far
+    above max(1, |features|) must not bias the fp half."""
+    B, E, hf, cin, emb = 3, 1, 16, 64, 128
+    P = synth.reference_state_dict(5, cin=cin, emb=emb, obj_bias=-0.2)
+    P["matcher.scale"] = torch.tensor([scale])
+    feats = synth.sam_features(31, B, cin, hf, hf)
+    ex, _ = synth.exemplar_set(32, B, E, 2 * hf, 2 * hf, 3, 9)
+    ui = np.repeat(np.arange(B), E)
+    res = {}
+    for share in (True, False):
+        eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=emb))
+        eng.share_fp_half = share  # U < 2B: unshared either way
+        r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
+        assert eng.last_shared_flops == 0.0
+        res[share] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
+        # max |f_TM| (fused in the xcorr kernel) lies exponents above max(1, |features|)
+        tm = [v[2] for k, v in eng._absmax_memo.items() if k[1] == "ftm"]
+        assert float(tm[0]) > 2.0 ** np.ceil(np.log2(max(1.0, float(np.abs(feats).max()))))
+    o, b = res[True]
+    for u in range(B * E):
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]),
+                                            [torch.from_numpy(ex.reshape(-1, 4)[u:u + 1])], P)
+        assert normwise(o[u], ro[0][0].numpy()) <= TOL, u
+        assert normwise(b[u], rb[0][0].numpy()) <= TOL, u
+
+
+def test_template_matching_module_api():
+    """matcher() is UNSCALED and forward() = matcher() * scale (template_matching.py:79-99);
+    cross_correlation / extract_function / matching_algorithm as the reference's."""
+    C, H, W = 32, 64, 64
+    f = synth.normal(40, (2, C, H, W))
+    boxes = np.stack([synth.exemplar_box(7, H, W, 3, 11), synth.exemplar_box(13, H, W, 20, 2)])
+    m = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    with torch.no_grad():
+        m.scale.fill_(0.37)
+    exl = [torch.from_numpy(b[None]).to(DEV) for b in boxes]
+    fd = cuda(f)
+    raw = m.matcher(fd, exl)
+    fwd = m(fd, exl)
+    assert bits_equal((raw * m.scale).detach().cpu().numpy(), fwd.detach().cpu().numpy())
+    for b in range(2):
+        roi, ht, wt = oracle.template_size(boxes[b], H, W)
+        t = oracle.roi_align(f[b], roi, ht, wt)
+        assert normwise(raw[b].cpu().numpy(), oracle.xcorr(f[b], t, 1.0)) <= TOL
+        # the members, called like the reference's matcher loop does (:86-88)
+        tg = m.extract_function(fd[b:b + 1], exl[b][0])
+        assert bits_equal(tg.cpu().numpy()[0], t)
+        cc = m.matching_algorithm(fd[b:b + 1], tg)
+        assert cc.shape == (1, C, H, W)
+        assert bits_equal(cc.cpu().numpy()[0], raw[b].cpu().numpy())
+    # a replaced member is honoured (the reference loop): identity "correlation"
+    m.matching_algorithm = lambda feat, tmpl: feat
+    assert bits_equal(m.matcher(fd, exl).cpu().numpy(), f)
+
+
+def _model_and_inputs(seed=11, B=1, E=3, hf=32, cin=64, emb=64, bias=-0.5):
+    args = SimpleNamespace(emb_dim=emb, fusion=True, ablation_no_box_regression=False,
+                           encoder="original", feature_upsample=True, no_matcher=False,
+                           template_type="roi_align", squeeze=False, decoder_num_layer=1,
+                           decoder_kernel_size=3, modeltype="matching_net", backbone="features",
+                           num_channels=cin, NMS_cls_threshold=0.3, NMS_iou_threshold=0.5)
+    model = tmr_amd.build_model(args)  # models/__init__.py:4 signature
+    P = synth.reference_state_dict(seed, cin=cin, emb=emb, obj_bias=bias)
+    model.load_state_dict(P, strict=True)
+    model = model.to(DEV).eval()
+    feats = synth.sam_features(seed + 1, B, cin, hf, hf)
+    ex, _ = synth.exemplar_set(seed + 2, B, E, 2 * hf, 2 * hf, 3, 11)
+    return args, model, P, feats, ex
+
+
+def test_demo_infer_call_form():
+    """demo.py:106-130, line for line: one model call per exemplar, Get_pred_boxes,
+    concat in exemplar order, one NMS."""
+    args, model, P, feats, ex = _model_and_inputs()
+    image = cuda(feats)  # the passthrough backbone's input = SAM features
+    scaled_exemplars = [cuda(ex[0])]
+    exemplars = [[e.unsqueeze(0)] for e in scaled_exemplars[0]]  # demo.py:106
+    pred_logits, pred_boxes, ref_points = [], [], []
+    maps = []
+    with torch.no_grad():
+        for exemplar in exemplars:  # demo.py:111
+            pred_objectness, pred_regressions, matching_feature, _ = model(image, exemplar)
+            dummy = {"regression_ablation_b": False, "regression_ablation_c": False}
+            _l, _b, _r = tmr_amd.Get_pred_boxes(pred_objectness, pred_regressions, exemplar, dummy,
+                                                args.NMS_cls_threshold, True)
+            pred_logits.append(_l[0]); pred_boxes.append(_b[0]); ref_points.append(_r[0])
+            maps.append((pred_objectness[0].cpu().numpy(), pred_regressions[0].cpu().numpy()))
+            assert matching_feature[0].shape == (1, args.emb_dim, 2 * feats.shape[-2], 2 * feats.shape[-1])
+    pred_logits = [torch.concat(pred_logits)]
+    pred_boxes = [torch.concat(pred_boxes)]
+    ref_points = [torch.concat(ref_points)]
+    pred_logits, pred_boxes, ref_points = tmr_amd.NMS(pred_logits, pred_boxes, ref_points,
+                                                      args.NMS_iou_threshold)
+    # the same sequence on the oracle: maps within 1e-5, detections bit-exact on the GPU's maps
+    Pc = {k: v.cpu() for k, v in P.items()}
+    for e in range(ex.shape[1]):
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats), [torch.from_numpy(ex[0, e:e + 1])], Pc)
+        assert normwise(maps[e][0], ro[0].numpy()) <= TOL
+        assert normwise(maps[e][1], rb[0].numpy()) <= TOL
+    gl, gb, gr = _oracle_detect_on_maps([oracle.sigmoid_cr(m[0][0, 0]) for m in maps],
+                                        [m[1][0] for m in maps], list(ex[0]),
+                                        args.NMS_cls_threshold, args.NMS_iou_threshold)
+    assert bits_equal(pred_logits[0].cpu().numpy(), gl)
+    assert bits_equal(pred_boxes[0].cpu().numpy(), gb)
+    assert bits_equal(ref_points[0].cpu().numpy(), gr)
+    assert pred_boxes[0].shape[0] >= 1
+
+
+def test_trainer_each_step_call_forms():
+    """trainer.py:123-150 (each_step, batch of 2, first exemplar of each) and
+    trainer.py:75-118 (each_step_multi_exemplars, batch 1, 3 exemplars)."""
+    args, model, P, feats, ex = _model_and_inputs(seed=21, B=2, E=3)
+    Pc = {k: v.cpu() for k, v in P.items()}
+    batch = {"image": cuda(feats), "exemplars": [cuda(ex[b]) for b in range(2)]}
+    batch["regression_ablation_a"] = False
+    batch["regression_ablation_b"] = False
+    batch["regression_ablation_c"] = False
+    with torch.no_grad():
+        po, pr, _, _ = model(batch["image"], batch["exemplars"])  # trainer.py:132
+        L, Bx, R = tmr_amd.Get_pred_boxes(po, pr, batch["exemplars"], batch, args.NMS_cls_threshold,
+                                          not batch["regression_ablation_a"])  # :144
+        L, Bx, R = tmr_amd.NMS(L, Bx, R, args.NMS_iou_threshold)  # :149
+    o, b = po[0].cpu().numpy(), pr[0].cpu().numpy()
+    for i in range(2):
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[i:i + 1]),
+                                            [torch.from_numpy(ex[i, :1])], Pc)
+        assert normwise(o[i], ro[0][0].numpy()) <= TOL
+        assert normwise(b[i], rb[0][0].numpy()) <= TOL
+        gl, gb, gr = _oracle_detect_on_maps([oracle.sigmoid_cr(o[i, 0])], [b[i]], [ex[i, 0]],
+                                            args.NMS_cls_threshold, args.NMS_iou_threshold)
+        assert bits_equal(Bx[i].cpu().numpy(), gb) and bits_equal(L[i].cpu().numpy(), gl)
+    # each_step_multi_exemplars: batch size 1, exemplars split one by one (:95-118)
+    multi = [cuda(ex[0])]
+    multi_exemplars = [[e.unsqueeze(0)] for e in multi[0]]
+    pl, pb, prf, maps = [], [], [], []
+    with torch.no_grad():
+        for exemplars in multi_exemplars:
+            po, pr, _, _ = model(batch["image"][:1], exemplars)
+            _l, _b, _r = tmr_amd.Get_pred_boxes(po, pr, exemplars, batch, args.NMS_cls_threshold, True)
+            pl.append(_l[0]); pb.append(_b[0]); prf.append(_r[0])
+            maps.append((oracle.sigmoid_cr(po[0].cpu().numpy()[0, 0]), pr[0].cpu().numpy()[0]))
+    pl, pb, prf = tmr_amd.NMS([torch.concat(pl)], [torch.concat(pb)], [torch.concat(prf)],
+                              args.NMS_iou_threshold)
+    gl, gb, gr = _oracle_detect_on_maps([m[0] for m in maps], [m[1] for m in maps], list(ex[0]),
+                                        args.NMS_cls_threshold, args.NMS_iou_threshold)
+    assert bits_equal(pl[0].cpu().numpy(), gl) and bits_equal(pb[0].cpu().numpy(), gb)
+    assert bits_equal(prf[0].cpu().numpy(), gr)
