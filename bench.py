@@ -102,6 +102,36 @@ def cpu_baseline(P, feats, ex, seconds: float, cls: float, iou: float):
                       f"{dt:.1f} s, torch {torch.__version__} CPU ({threads} threads)"}
 
 
+def xcorr_by_class(eng, feats_d, ex, reps: int = 3):
+    """The correlation kernel per template class (k <= 9: HBM-bound, k >= 11:
+    VALU/MFMA-bound), each class's units of the batch in one
+    tmr_xcorr launch, timed with HIP events on the launch stream (outside
+    the timed region)."""
+    from tmr_amd import host as _host
+    B, E = ex.shape[:2]
+    boxes = ex.reshape(-1, 4)
+    ui = np.repeat(np.arange(B), E)
+    fp, _ = eng.project(feats_d)
+    Hm, Wm = fp.shape[-2:]
+    ks = np.array([max(_host.template_size(b, Hm, Wm)[1:]) for b in boxes])
+    out = {}
+    for name, sel in (("k<=9", ks <= 9), ("k>=11", ks >= 11)):
+        if not sel.any():
+            continue
+        eng.xcorr_events = []
+        for _ in range(reps):
+            eng.match(fp, ui[sel], boxes[sel])
+        torch.cuda.synchronize()
+        xs = float(np.mean([s_.elapsed_time(e_) for s_, e_ in eng.xcorr_events])) / 1e3
+        eng.xcorr_events = None
+        out[name] = {"units": int(sel.sum()), "avg_launch_ms": round(1e3 * xs, 3),
+                     "hbm_achieved": round(eng.last_xcorr_bytes / xs / 1e9, 1),
+                     "hbm_frac": round(eng.last_xcorr_bytes / xs / 1e9 / HBM_PEAK_GBS, 4),
+                     "valu_achieved": round(eng.last_xcorr_flops / xs / 1e12, 2),
+                     "valu_frac": round(eng.last_xcorr_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4)}
+    return out
+
+
 def load_traffic(algo: str, prec: str):
     """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, raw) of the decoder
     kernel from the committed rocprofv3 PMC summary of the current kernel
@@ -127,6 +157,9 @@ def main():
     ap.add_argument("--precision", default=None, choices=sorted(SPLIT_TERMS),
                     help="decoder arithmetic (default: the config's; fp32 = 3-term fp16 split)")
     ap.add_argument("--decoder", default="split", choices=["split", "wino", "direct"])
+    ap.add_argument("--path", default="detect", choices=["detect", "module"],
+                    help="detect: TMREngine.detect over the batch (B x E units per launch); module: "
+                         "the reference's per-exemplar module calls (demo.py:106-130)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
@@ -157,15 +190,49 @@ def main():
     ex, _ = synth.exemplar_set(2000 + rank, B, E, H, W, cfg["kmin"], cfg["kmax"])
     feats_d = torch.from_numpy(feats).to(dev)
 
-    def step():
-        L, Bx, R = eng.detect(feats_d, ex, cls_ths=cfg["cls"], iou_threshold=cfg["iou"])
-        if world > 1:
-            counts, rows = driver.pack_rows(L, Bx, R)
-            driver.all_gather_detections(counts, rows)
-        return L
+    if a.path == "module":
+        # the reference's module-level call sequence, line for line
+        # (demo.py:106-130): one matching_net forward per exemplar (with its
+        # relu(f_TM) and f[0] outputs), Get_pred_boxes, concat, one NMS
+        from types import SimpleNamespace
+        margs = SimpleNamespace(emb_dim=EMB, fusion=True, ablation_no_box_regression=False,
+                                encoder="original", feature_upsample=True, no_matcher=False,
+                                template_type="roi_align", squeeze=False, decoder_num_layer=1,
+                                decoder_kernel_size=KS, modeltype="matching_net", backbone="features",
+                                num_channels=CIN, precision=prec)
+        model = tmr.build_model(margs)
+        model.load_state_dict(P, strict=True)
+        model = model.to(dev).eval()
+        ex_d = torch.from_numpy(ex).to(dev)
+        per_image = [[[ex_d[b, e].unsqueeze(0)] for e in range(E)] for b in range(B)]  # demo.py:106
+        dummy = {"regression_ablation_b": False, "regression_ablation_c": False}
+
+        def step():
+            out = []
+            with torch.no_grad():
+                for b in range(B):
+                    image = feats_d[b:b + 1]
+                    pl, pb, pr = [], [], []
+                    for exemplar in per_image[b]:
+                        po, preg, _, _ = model(image, exemplar)
+                        _l, _b, _r = tmr.Get_pred_boxes(po, preg, exemplar, dummy, cfg["cls"], True)
+                        pl.append(_l[0]); pb.append(_b[0]); pr.append(_r[0])
+                    L_, _, _ = tmr.NMS([torch.concat(pl)], [torch.concat(pb)], [torch.concat(pr)],
+                                       cfg["iou"])
+                    out.append(L_[0])
+            return out
+    else:
+        def step():
+            L, Bx, R = eng.detect(feats_d, ex, cls_ths=cfg["cls"], iou_threshold=cfg["iou"])
+            if world > 1:
+                counts, rows = driver.pack_rows(L, Bx, R)
+                driver.all_gather_detections(counts, rows)
+            return L
 
     for _ in range(a.warmup):
         step()
+    if a.path == "module":
+        eng = model.engine()  # the module's engine: its launches are the timed ones
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -194,10 +261,6 @@ def main():
         flops = eng.last_decoder_flops  # executed FLOPs of the timed launch
         avg_s = float(np.mean(dec_ms)) / 1e3
         achieved = flops / avg_s / 1e12
-        # the per-unit f_TM half as a direct 3x3 conv: 2*H*W*N*(512*9) per unit
-        direct_equiv = 2.0 * H * W * (4 * EMB) * (EMB * KS * KS) * B * E
-        if eng.last_shared_flops == 0.0:  # unshared (E == 1): the launch covers both halves
-            direct_equiv *= 2
         algo = eng.last_decoder_algo
         peak, terms = FP32_PEAK_TFLOPS, 1
         if algo == "split":
@@ -220,7 +283,17 @@ def main():
         else:
             kernel_name = "tmr_conv_heads (direct decoder_b+decoder_o f_TM half + heads)"
             flops_basis = "executed: 2*H*W*N(2048)*K(512*9) per unit (f_TM half)"
-        achieved *= terms
+        executed_achieved = achieved * terms
+        # SURVEY.md 8d algorithmic FLOPs of the timed launch: the decoder
+        # convs' f_TM half, 2*H*W*2048*(512*9) per unit (both halves when the
+        # fp half is not shared, E = 1), independent of how the kernel
+        # executes them (3-term split, folded projection, ...)
+        units_per_launch = B * E if a.path == "detect" else 1
+        alg_flops = 2.0 * H * W * (4 * EMB) * (EMB * KS * KS) * units_per_launch
+        if eng.last_shared_flops == 0.0:
+            alg_flops *= 2
+        alg_achieved = alg_flops / avg_s / 1e12
+        path_alg = decoder_flops_per_unit() * B * E  # both decoders, whole path per step
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
@@ -231,15 +304,21 @@ def main():
                        "images_per_gpu": B, "exemplars": E, "feature": [CIN, H // 2, W // 2],
                        "matching_map": [EMB, H, W], "parallelism": f"dp{world}",
                        "mean_kept_per_image": round(float(np.mean(kept)), 1),
-                       "decoder": algo, "decoder_precision": prec},
+                       "decoder": algo, "decoder_precision": prec, "path": a.path},
             "roofline": {"bound": "mfma", "kernel": kernel_name,
-                         "achieved": round(achieved, 2), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "achieved": round(alg_achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(alg_achieved / peak, 4),
                          "traffic": load_traffic(algo, prec), "avg_launch_ms": round(1e3 * avg_s, 3),
-                         "flops_per_launch": flops * terms, "flops_basis": flops_basis,
-                         "direct_conv_equivalent_tflops": round(direct_equiv / avg_s / 1e12, 2),
-                         "path_algorithmic_tflop_per_step": round(
-                             decoder_flops_per_unit() * B * E / 1e12, 2)},
+                         "flops_per_launch": alg_flops,
+                         "flops_basis": "algorithmic (SURVEY.md 8d): 2*H*W*N(2048)*K(512*9) per unit, the "
+                                        "decoder_b+decoder_o conv over the f_TM half (x2 when E=1: both "
+                                         "halves in this launch); peak = dense 16-bit MFMA",
+                         "executed_achieved": round(executed_achieved, 2),
+                         "executed_frac": round(executed_achieved / peak, 4),
+                         "executed_basis": flops_basis,
+                         "path_algorithmic_tflop_per_step": round(path_alg / 1e12, 2),
+                         "path_achieved": round(path_alg / (ms_step / 1e3) / 1e12, 2),
+                         "path_frac": round(path_alg / (ms_step / 1e3) / 1e12 / peak, 4)},
         }
         # the correlation kernel (SURVEY.md 8d "kernel 2"): HBM-bound for small
         # templates, VALU-bound for k >= 11; both fractions, algorithmic work
@@ -253,7 +332,8 @@ def main():
             "valu_achieved": round(eng.last_xcorr_flops / xs / 1e12, 2), "valu_peak": FP32_PEAK_TFLOPS,
             "valu_unit": "TFLOP/s", "valu_frac": round(eng.last_xcorr_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4),
             "basis": "per unit: read + write C*H*W fp32 (the fp plane read once per unit, f_TM written), "
-                     "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)"}
+                     "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)",
+            "by_class": xcorr_by_class(eng, feats_d, ex)}
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds, cfg["cls"], cfg["iou"])
         else:

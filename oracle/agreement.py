@@ -77,27 +77,23 @@ def compare(maps_a: Sequence, maps_b: Sequence, boxes: Sequence, thr: float, iou
     ib = np.array([pos_b[ids_a[i]] for i in common], np.int64)
     order_flips = iou_flips = 0
     iou_margin = 0.0
-    if ia.size and ia.size <= 12000:
-        sa, sb = La[ia, 0], Lb[ib, 0]
-        # stable descending sort: i before j iff s_i > s_j or (== and earlier row)
-        before_a = (sa[:, None] > sa[None]) | ((sa[:, None] == sa[None]) & (ia[:, None] < ia[None]))
-        before_b = (sb[:, None] > sb[None]) | ((sb[:, None] == sb[None]) & (ib[:, None] < ib[None]))
-        order_flips = int(np.triu(before_a != before_b, 1).sum())
-        qa, qb = _iou_matrix(Ba[ia]), _iou_matrix(Bb[ib])
-        fl = np.triu((qa.astype(np.float64) > iou) != (qb.astype(np.float64) > iou), 1)
-        iou_flips = int(fl.sum())
-        if iou_flips:
-            iou_margin = float(np.abs(qa[fl].astype(np.float64) - iou).max())
+    if ia.size:
+        order_flips, iou_flips, iou_margin = oracle.decision_flips(
+            Ba[ia], La[ia, 0], ia, Bb[ib], Lb[ib, 0], ib, iou)
     first_div = next((i for i, (x, y) in enumerate(zip(kid_a, kid_b)) if x != y),
                      None if len(kid_a) == len(kid_b) else min(len(kid_a), len(kid_b)))
     sa_set, sb_set = set(kid_a), set(kid_b)
     inter = sa_set & sb_set
-    # matched-box IoU: each kept box of run a against its best kept box of run b
-    best = np.zeros(0)
+    # matched-box IoU: each kept box of run a against the same candidate's kept
+    # box in run b, or (kept by a only) its best kept box of run b
+    best = np.zeros(len(keep_a))
     if len(keep_a) and len(keep_b):
-        ka, kb = Ba[keep_a], Bb[keep_b]
-        qab = _iou_matrix(np.concatenate([ka, kb]))[: len(ka), len(ka):]
-        best = np.nan_to_num(qab, nan=0.0).max(1)
+        kpos_b = {k: i for i, k in enumerate(kid_b)}
+        kb = Bb[keep_b]
+        for i, k in enumerate(kid_a):
+            a = Ba[keep_a[i]][None]
+            cand = kb[kpos_b[k]][None] if k in kpos_b else kb
+            best[i] = float(np.nan_to_num(_iou_matrix(np.concatenate([a, cand]))[0, 1:], nan=0.0).max())
     same_ids = kid_a == kid_b
     box_diff = float(np.abs(Ba[keep_a] - Bb[keep_b]).max()) if same_ids and len(keep_a) else 0.0
     return dict(

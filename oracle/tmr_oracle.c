@@ -359,4 +359,49 @@ int64_t orc_nms(const float *boxes, const float *scores, int64_t n, double thr, 
     return nk;
 }
 
+/* Test-infrastructure helper for oracle/agreement.py: over the n candidates two
+ * runs share (row i of a and of b is the same (unit, pixel)), count the pairs
+ * whose NMS sort order (stable descending, by the run's own row positions) or
+ * IoU decision ((double)IoU > thr, the arithmetic of orc_nms) differ between
+ * the runs.  margin[0] = max |IoU_a - thr| over the IoU flips. */
+static float iou_f32(const float *bi, const float *bj) {
+    float ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+    float aj = (bj[2] - bj[0]) * (bj[3] - bj[1]);
+    float xx1 = bi[0] > bj[0] ? bi[0] : bj[0];
+    float yy1 = bi[1] > bj[1] ? bi[1] : bj[1];
+    float xx2 = bi[2] < bj[2] ? bi[2] : bj[2];
+    float yy2 = bi[3] < bj[3] ? bi[3] : bj[3];
+    float w = xx2 - xx1; if (!(w > 0.0f)) w = 0.0f;
+    float h = yy2 - yy1; if (!(h > 0.0f)) h = 0.0f;
+    float inter = w * h;
+    return inter / (ai + aj - inter);
+}
+
+void orc_decision_flips(int64_t n, const float *boxes_a, const float *scores_a, const int64_t *rows_a,
+                        const float *boxes_b, const float *scores_b, const int64_t *rows_b, double thr,
+                        int64_t *order_flips, int64_t *iou_flips, double *margin) {
+    int64_t of = 0, qf = 0;
+    double mg = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = i + 1; j < n; ++j) {
+            int ba = scores_a[i] > scores_a[j] || (scores_a[i] == scores_a[j] && rows_a[i] < rows_a[j]);
+            int bb = scores_b[i] > scores_b[j] || (scores_b[i] == scores_b[j] && rows_b[i] < rows_b[j]);
+            of += ba != bb;
+            const float *ai = boxes_a + 4 * i, *aj = boxes_a + 4 * j;
+            const float *bi = boxes_b + 4 * i, *bj = boxes_b + 4 * j;
+            /* no overlap in either run: both IoUs are 0 */
+            if (!(ai[0] < aj[2] && aj[0] < ai[2] && ai[1] < aj[3] && aj[1] < ai[3]) &&
+                !(bi[0] < bj[2] && bj[0] < bi[2] && bi[1] < bj[3] && bj[1] < bi[3]))
+                continue;
+            double qa = (double)iou_f32(ai, aj), qb = (double)iou_f32(bi, bj);
+            if ((qa > thr) != (qb > thr)) {
+                ++qf;
+                double d = qa > thr ? qa - thr : thr - qa;
+                if (d > mg) mg = d;
+            }
+        }
+    }
+    *order_flips = of; *iou_flips = qf; *margin = mg;
+}
+
 int orc_version(void) { return 1; }
