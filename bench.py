@@ -124,11 +124,13 @@ def xcorr_by_class(eng, feats_d, ex, reps: int = 3):
         torch.cuda.synchronize()
         xs = float(np.mean([s_.elapsed_time(e_) for s_, e_ in eng.xcorr_events])) / 1e3
         eng.xcorr_events = None
-        out[name] = {"units": int(sel.sum()), "avg_launch_ms": round(1e3 * xs, 3),
+        out[name] = {"units": int(sel.sum()), "algo": eng.last_xcorr_algo, "avg_launch_ms": round(1e3 * xs, 3),
                      "hbm_achieved": round(eng.last_xcorr_bytes / xs / 1e9, 1),
                      "hbm_frac": round(eng.last_xcorr_bytes / xs / 1e9 / HBM_PEAK_GBS, 4),
                      "valu_achieved": round(eng.last_xcorr_flops / xs / 1e12, 2),
                      "valu_frac": round(eng.last_xcorr_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        if eng.last_xcorr_algo == "mfma":  # the unit it runs on: dense 16-bit MFMA
+            out[name]["mfma_frac"] = round(eng.last_xcorr_flops / xs / 1e12 / F16_PEAK_TFLOPS, 4)
     return out
 
 
@@ -323,8 +325,14 @@ def main():
         # the correlation kernel (SURVEY.md 8d "kernel 2"): HBM-bound for small
         # templates, VALU-bound for k >= 11; both fractions, algorithmic work
         xs = float(np.mean(xc_ms)) / 1e3
+        xk = eng.last_xcorr_algo
         out["roofline_xcorr"] = {
-            "kernel": "tmr_xcorr (xcorr_rows_kernel: depthwise xcorr + /hw + pad + scale + max|f_TM|)",
+            "kernel": ("tmr_xcorr_algo MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
+                       "v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if xk == "mfma" else
+                       "tmr_xcorr_algo VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
+                      + " + /hw + pad + scale + max|f_TM|; kernel chosen by the measured per-k cost model "
+                        "(engine.XCORR_COST)",
+            "algo": xk,
             "bound": "hbm" if cfg["kmax"] <= 9 else "valu",
             "avg_launch_ms": round(1e3 * xs, 3),
             "hbm_achieved": round(eng.last_xcorr_bytes / xs / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,

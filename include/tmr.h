@@ -49,6 +49,9 @@ typedef struct tmr_unit {
     float roi[4];          /* roi_align box in feature px (x1,y1,x2,y2), :61-63   */
     int32_t pbox[4];       /* prototype snapped box (x1,y1,x2,y2), :49-50         */
     int64_t tmpl_offset;   /* float offset of this unit's [C,ht,wt] template      */
+    int32_t row_offset;    /* sum of ht over the units before this one (the MFMA  */
+                           /* correlation's split-template rows, tmr_template_split) */
+    int32_t pad_;
 } tmr_unit_t;
 
 /* Per-unit peak-finder parameters (utils/TM_utils.py:236-278). */
@@ -106,6 +109,36 @@ int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates
               const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
               const float *scale, int squeeze, float *out, float *relu_out, float *work,
               float *out_absmax, void *stream);
+/* Same operation with the kernel chosen explicitly: TMR_XCORR_VALU (fp32
+ * LDS-blocked wavefront kernels), TMR_XCORR_MFMA (row-Toeplitz implicit GEMM
+ * on v_mfma_f32_16x16x32_f16 with the fp32-grade 3-term split: W % 32 == 0,
+ * W <= 256, templates <= 31x31, needs tmpl_split; TMR_E_UNSUPPORTED
+ * otherwise) or TMR_XCORR_AUTO (MFMA when the shape fits it, tmpl_split is
+ * given and min_k -- the smallest template side in the launch -- reaches the
+ * counter-chosen crossover; VALU otherwise).  tmpl_split
+ * (nullable) holds tmr_template_split(templates, ..., total_rows, ...) of the
+ * same templates.  tmr_xcorr(...) runs the VALU kernels. */
+#define TMR_XCORR_AUTO 0
+#define TMR_XCORR_VALU 1
+#define TMR_XCORR_MFMA 2
+int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
+                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
+                   const float *scale, int squeeze, float *out, float *relu_out, float *work,
+                   float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
+                   int min_k, void *stream);
+/* Operand prep of the MFMA correlation: per (unit u, channel c) template
+ * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
+ * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <
+ * 2^14), written as zero-padded rows (TMR_TSPLIT_ROW fp16 each, tap j at
+ * column TMR_TSPLIT_PAD + j): row i of term k (0 hi, 1 lo) of (u, c) is row
+ * (C * row_offset(u) + c * ht) * 2 + k * ht + i; then e int32[U][C].
+ * total_rows = sum of ht over the units; size in bytes from
+ * tmr_template_split_size. */
+#define TMR_TSPLIT_ROW 96
+#define TMR_TSPLIT_PAD 24
+int64_t tmr_template_split_size(int U, int C, int64_t total_rows);
+int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
+                       int64_t total_rows, void *out, void *stream);
 
 /* ---- (a10+a11+a12) conv stack ---------------------------------------------
  * Implicit-GEMM kxk conv over the virtual channel concat

@@ -1,10 +1,13 @@
-"""Micro-benchmark of the correlation step at the config-B shape: 64 images x
-3 exemplars, fp [64,512,128,128], templates 3..15 (TMREngine.match =
-tmr_templates + tmr_xcorr with the fused max |f_TM|).  HIP events on the
-launch stream, median of R repetitions; prints one JSON line with the VALU
-roofline fraction (2*C*(H-h+1)(W-w+1)*h*w flops per unit, 157.3 TF fp32).
+"""Micro-benchmark of the correlation kernel (tmr_xcorr_algo) per template
+size and kernel: for each k, B images x E exemplars of k x k templates on
+fp [B,512,H,H]; HIP events around the xcorr launch on its stream (median of
+R repetitions).  One JSON line per (algo, k) with the SURVEY.md 8d roofline
+figures: algorithmic bytes = read + write C*H*W fp32 per unit (fp read once
+per unit, f_TM written), FLOPs = 2*C*(H-k+1)^2*k^2 per unit; HBM peak 8 TB/s,
+fp32 VALU peak 157.3 TF.  --mixed runs the config-B mix (k uniform 3..15).
 
-    python profiles/kbench_xcorr.py [--images 64] [--reps 5]
+    python profiles/kbench_xcorr.py [--images 64] [--E 3] [--H 128] [--algos valu,mfma]
+                                    [--ks 1,3,5,...] [--mixed]
 """
 import argparse
 import json
@@ -22,41 +25,59 @@ tmr = load_package()
 from tmr_amd import synth  # noqa: E402
 
 
+def run(eng, fp, ui, boxes, reps):
+    eng.match(fp, ui, boxes)  # warm
+    eng.xcorr_events = []
+    for _ in range(reps):
+        eng.match(fp, ui, boxes)
+    torch.cuda.synchronize()
+    ms = float(np.median([s.elapsed_time(e) for s, e in eng.xcorr_events]))
+    eng.xcorr_events = None
+    return ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=64)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--E", type=int, default=3)
-    ap.add_argument("--kmax", type=int, default=15)
+    ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--algos", default="valu,mfma")
+    ap.add_argument("--ks", default="1,3,5,7,9,11,13,15,17,21,25,31")
+    ap.add_argument("--mixed", action="store_true", help="config-B mix: k uniform over 3..15")
     ap.add_argument("--kmin", type=int, default=3)
+    ap.add_argument("--kmax", type=int, default=15)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    B, C, H = a.images, 512, 128
+    B, C, H = a.images, 512, a.H
     P = {k: v.to(dev) for k, v in synth.reference_state_dict(0).items()}
     eng = tmr.TMREngine(P, tmr.PathConfig())
     g = torch.Generator(device=dev).manual_seed(0)
     fp = torch.randn((B, C, H, H), device=dev, generator=g)
-    ex, ks = synth.exemplar_set(1, B, a.E, H, H, a.kmin, a.kmax)
     ui = np.repeat(np.arange(B), a.E)
-    boxes = ex.reshape(-1, 4)
-    flops = 0.0
-    for k in np.asarray(ks).reshape(-1):
-        k = int(k)
-        flops += 2.0 * C * (H - k + 1) ** 2 * k * k
-    eng.match(fp, ui, boxes)
-    ts = []
-    for _ in range(a.reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        eng.match(fp, ui, boxes)
-        e.record()
-        torch.cuda.synchronize()
-        ts.append(s.elapsed_time(e))
-    ms = float(np.median(ts))
-    out_bytes = B * a.E * C * H * H * 4
-    print(json.dumps({"images": B, "E": a.E, "k": [a.kmin, a.kmax], "ms": round(ms, 3), "gflop": round(flops / 1e9, 1),
-                      "tflops": round(flops / ms / 1e9, 1), "frac_valu": round(flops / ms / 1e9 / 157.3, 3),
-                      "hbm_gbps_out": round(out_bytes / ms / 1e6, 1)}))
+    sets = []
+    if a.mixed:
+        ex, ks = synth.exemplar_set(1, B, a.E, H, H, a.kmin, a.kmax)
+        sets.append((f"{a.kmin}..{a.kmax}", ex.reshape(-1, 4), np.asarray(ks).reshape(-1)))
+    else:
+        for k in [int(x) for x in a.ks.split(",")]:
+            ex, ks = synth.exemplar_set(1, B, a.E, H, H, k, k)
+            sets.append((str(k), ex.reshape(-1, 4), np.asarray(ks).reshape(-1)))
+    for name, boxes, ks in sets:
+        flops = float(sum(2.0 * C * (H - k + 1) ** 2 * k * k for k in ks))
+        nbytes = 2.0 * 4 * C * H * H * len(ks)
+        for algo in a.algos.split(","):
+            eng.xcorr_algo = algo
+            try:
+                ms = run(eng, fp, ui, boxes, a.reps)
+            except tmr.TMRError as e:
+                print(json.dumps({"algo": algo, "k": name, "error": str(e)}), flush=True)
+                continue
+            print(json.dumps({"algo": algo, "k": name, "images": B, "E": a.E, "H": H, "ms": round(ms, 4),
+                              "hbm_gbps": round(nbytes / ms / 1e6, 1),
+                              "hbm_frac": round(nbytes / ms / 1e6 / 8000.0, 4),
+                              "tflops": round(flops / ms / 1e9, 2),
+                              "valu_frac": round(flops / ms / 1e9 / 157.3, 4)}), flush=True)
 
 
 if __name__ == "__main__":

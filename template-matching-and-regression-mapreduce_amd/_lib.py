@@ -24,10 +24,11 @@ _lib = None
 
 # ABI structs (must match include/tmr.h)
 UNIT_DTYPE = np.dtype({
-    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset"],
-    "formats": [np.int32, np.int32, np.int32, np.int32, (np.float32, 4), (np.int32, 4), np.int64],
-    "offsets": [0, 4, 8, 12, 16, 32, 48],
-    "itemsize": 56,
+    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset", "row_offset"],
+    "formats": [np.int32, np.int32, np.int32, np.int32, (np.float32, 4), (np.int32, 4), np.int64,
+                np.int32],
+    "offsets": [0, 4, 8, 12, 16, 32, 48, 56],
+    "itemsize": 64,
 })
 PEAK_DTYPE = np.dtype({
     "names": ["thr", "scale_w", "scale_h", "mask", "mode", "pad_"],
@@ -42,6 +43,8 @@ TEMPLATE_PROTOTYPE = 1
 # decoder-conv precision modes of the split 16-bit-MFMA kernel (include/tmr.h)
 PREC_CODES = {"fp32": 0, "bf16": 1, "f16": 2}
 SPLIT_TILED_OUT, SPLIT_TILED_INIT, SPLIT_INIT_BCAST = 1, 2, 4
+# correlation kernel choice (tmr_xcorr_algo)
+XCORR_ALGOS = {"auto": 0, "valu": 1, "mfma": 2}
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -57,6 +60,10 @@ SIGNATURES = {
     "tmr_upsample_proj": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P]),
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
+    "tmr_xcorr_algo": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
+                            _I, _I, _P]),
+    "tmr_template_split_size": (_L, [_I, _I, _L]),
+    "tmr_template_split": (_I, [_P, _P, _I, _I, _L, _P, _P]),  # (..., total_rows, out, stream)
     "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
     "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),

@@ -23,6 +23,8 @@
 // taps preloaded for 3x3: no change; for 5x5 the 25 taps spill SGPRs.)  The
 // divide by fl32(h*w) is correctly
 // rounded (div_cr), bit-identical to the reference's `/ (h*w + 1e-14)`.
+#include <algorithm>
+
 #include "tmr_common.h"
 
 namespace {
@@ -432,6 +434,293 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// MFMA variant (kernel (2) of BASELINE north_star): the depthwise correlation
+// as a row-Toeplitz GEMM on v_mfma_f32_16x16x32_f16 with an fp32-grade
+// 3-term split (the decoder's F16X3 scheme, conv_split.hip).
+//
+// For channel c, template row i and a 16x16 output tile at (y0, x0):
+//   D[m][n] = sum_k A_i[m][k] B_i[k][n],  m = output col x0+m, n = output row
+//   y0+n, k = input col a0+k (a0 = x0 - pw_al, pw_al = 8*ceil(pw/8)),
+//   A_i[m][k] = T[i][k - m - s]  (s = pw_al - pw; zero outside [0, w)),
+//   B_i[k][n] = F[y0 + n - ph + i][a0 + k],
+// summed over i = 0..h-1 (the template rows) into one accumulator; K per row
+// is 32 * NK with NK = ceil((16 + s + w - 1) / 32) (1 for w <= 17, 2 to 31).
+// Both operands are split x*s_x = xh + xl (fp16, power-of-two scales: the
+// staged band's max for F, the template's max for T) and every product is
+// th*fh + th*fl + tl*fh with fp32 accumulation (dropped tl*fl and the split
+// residuals ~2^-22 relative), then exactly unscaled, divided by fl32(h*w)
+// correctly rounded and scaled like the VALU kernels.
+//
+// Block = (band of 32 output rows, channel, image), 4 waves; the band's input
+// rows (+- the largest template's half height, zero rows outside the image,
+// zero columns left/right) are staged ONCE as fp16 hi/lo planes and reused
+// by every exemplar unit of the image.  Wave w owns tile row (w & 1) and every
+// other 16-col tile: its A (template) fragments are built once per template
+// row and reused across its NTW tiles.  LDS row stride SB = 32 mod 64 bytes
+// makes the B-fragment reads (16 lanes = 16 rows, same column) conflict free
+// for all four ds_read_b128 lane groups.  The 1-D grid is remapped so each
+// XCD runs a contiguous range of (band, channel, image) blocks: neighbouring
+// bands' halo rows meet in that XCD's L2.
+constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
+constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct MArgs {
+    int SB;     // LDS plane row stride in bytes (32 mod 64)
+    int LR;     // staged rows: band rows + 2 * HG
+    int HG;     // max template height / 2
+    int HTM;    // max template height (template LDS rows per term)
+    int nband;  // bands per channel plane
+    int nlog;   // logical blocks = nband * C * B
+};
+
+__device__ __forceinline__ float pow2_scale(float m, int &e) {
+    // s = 2^(14 - e') with m < 2^e' (max |x s| < 2^14); e = -log2(s)
+    if (!(m > 0.0f && m <= 3.0e38f)) { e = 0; return 1.0f; }
+    int ex;
+    frexpf(m, &ex);
+    e = ex - 14;
+    return ldexpf(1.0f, 14 - ex);
+}
+
+__device__ __forceinline__ float block_max(float v, float *red) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// Per (unit, channel) split of the exemplar templates for the MFMA kernel
+// (tmr_template_split): t * 2^-et = th + tl (fp16) with 2^-et the power-of-two
+// scale of the template's own max |t| (max |t| 2^-et < 2^14), written as
+// zero-padded rows so that the kernel's A fragment -- 8 consecutive taps
+// T[i][8g + 32nk - m - s ..] for lane (m, g) -- is ONE 16-B load per lane
+// with no bounds checks.  One wave per (unit, channel).
+constexpr int TROW = TMR_TSPLIT_ROW;
+constexpr int TOFF = TMR_TSPLIT_PAD;
+static_assert(TOFF >= 15 + 7 && TOFF + 64 + 8 <= TROW, "padded template rows");
+
+__global__ __launch_bounds__(256) void template_split_kernel(const float *__restrict__ tmpl,
+                                                             const tmr_unit_t *__restrict__ units, int U,
+                                                             int C, int64_t total_rows,
+                                                             _Float16 *__restrict__ rows,
+                                                             int32_t *__restrict__ exps) {
+    const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wid >= (int64_t)U * C) return;  // wave-uniform
+    const int u = (int)(wid / C), c = (int)(wid % C);
+    const tmr_unit_t un = units[u];
+    const int h = un.ht, w = un.wt, hw = h * w;
+    const float *t = tmpl + un.tmpl_offset + (int64_t)c * hw;
+    float m = 0.0f;
+    for (int e = lane; e < hw; e += 64) m = fmaxf(m, fabsf(t[e]));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    int et;
+    const float st = pow2_scale(m, et);
+    _Float16 *dst = rows + ((int64_t)C * un.row_offset + (int64_t)c * h) * 2 * TROW;
+    for (int e = lane; e < 2 * h * TROW; e += 64) {
+        const int term = e >= h * TROW, r = e - term * h * TROW, i = r / TROW, j = r % TROW - TOFF;
+        const float x = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
+        const _Float16 hx = (_Float16)x;
+        dst[e] = term ? (_Float16)(x - (float)hx) : hx;
+    }
+    if (lane == 0) exps[(int64_t)u * C + c] = et;
+}
+
+// one unit over the band: acc[t] += sum_i A_i B_i over the wave's NTW tiles
+// (tile cols tcol0 + WPR t).  The A fragments -- lane (m, g): taps
+// T[i][8g + 32nk + q - m - s], q = 0..7 -- are single 16-B (2-B aligned)
+// global loads from the zero-padded split rows (L2 resident), issued PF
+// template rows ahead of their MFMAs.  (Measured: staging them through an
+// LDS table per row chunk, with its two barriers per chunk, was slower at
+// every k >= 11; profiles/r02b_kbench_xcorr_*.)
+template <int NTW, int NK, int WPR>
+__device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
+                                          int h, const char *arow, int tcol0, int pw_al, int g) {
+    constexpr int PF = 1;  // prefetch distance (template rows; 2 costs a wave per SIMD in VGPRs)
+    h8 ah[PF][NK], al[PF][NK];
+    const size_t tstride = (size_t)h * TROW * 2;  // bytes from the hi rows to the lo rows
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < h) {
+#pragma unroll
+            for (int nk = 0; nk < NK; ++nk) {
+                ah[p][nk] = *reinterpret_cast<const h8 *>(arow + (size_t)p * TROW * 2 + 64 * nk);
+                al[p][nk] = *reinterpret_cast<const h8 *>(arow + tstride + (size_t)p * TROW * 2 + 64 * nk);
+            }
+        }
+    for (int i0 = 0; i0 < h; i0 += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int i = i0 + p;
+            if (i >= h) break;
+            const char *rh = Fh + (size_t)(rb + i) * SB, *rl = Fl + (size_t)(rb + i) * SB;
+            h8 ch[NK], cl[NK];
+#pragma unroll
+            for (int nk = 0; nk < NK; ++nk) {
+                ch[nk] = ah[p][nk];
+                cl[nk] = al[p][nk];
+            }
+            if (i + PF < h) {
+#pragma unroll
+                for (int nk = 0; nk < NK; ++nk) {
+                    ah[p][nk] = *reinterpret_cast<const h8 *>(arow + (size_t)(i + PF) * TROW * 2 + 64 * nk);
+                    al[p][nk] = *reinterpret_cast<const h8 *>(arow + tstride + (size_t)(i + PF) * TROW * 2 + 64 * nk);
+                }
+            }
+#pragma unroll
+            for (int nk = 0; nk < NK; ++nk) {
+#pragma unroll
+                for (int t = 0; t < NTW; ++t) {
+                    const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
+                    const h8 bh = *reinterpret_cast<const h8 *>(rh + colb);
+                    const h8 bl = *reinterpret_cast<const h8 *>(rl + colb);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[nk], bh, acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[nk], bl, acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl[nk], bh, acc[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+}
+
+template <int NTW, int NV4, int TRB>
+__global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
+                                                       const int32_t *__restrict__ texp,
+                                                       float *__restrict__ outp,
+                                                       const tmr_unit_t *__restrict__ units) {
+    constexpr int WPR = 4 / TRB;  // waves per tile row
+    constexpr int BR = 16 * TRB;  // output rows per block
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // XCD-aware map: hardware block L runs on XCD L % 8; give each XCD a
+    // contiguous range of logical blocks (band fastest)
+    const int L = blockIdx.x, per = gridDim.x >> 3;
+    const int q = (L & 7) * per + (L >> 3);
+    if (q >= m.nlog) return;
+    const int band = q % m.nband, c = (q / m.nband) % a.C, img = q / (m.nband * a.C);
+    const int H = a.H, W = a.W, SB = m.SB, LR = m.LR, hg = m.HG;
+    const int u_beg = __builtin_amdgcn_readfirstlane(a.img_units[img]);
+    const int u_end = __builtin_amdgcn_readfirstlane(a.img_units[img + 1]);
+    if (u_beg >= u_end) return;
+    char *Fh = smem, *Fl = smem + (size_t)LR * SB;
+    float *red = reinterpret_cast<float *>(smem + 2 * (size_t)LR * SB);
+    const int tid = threadIdx.x;
+    const int yb0 = band * BR, yb1 = min(yb0 + BR, H);
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    const float sc = a.squeeze ? 1.0f : *a.scale;
+
+    // ---- stage the band: fp32 -> registers -> block max -> fp16 hi/lo planes
+    const int W4 = W >> 2, n4 = LR * W4;
+    const float rw4 = 1.0f / (float)W4;  // e / W4 by one multiply (exact for e < 2^16)
+    float4 v[NV4];
+    float vm = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NV4; ++k) {
+        const int e = tid + k * NT;
+        v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
+        const int yy = yb0 - hg + lr;
+        if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
+    }
+    // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
+    {
+        const int pr = SB / 16 - W / 8;   // 16-B pieces of pad per row (2 left, rest right)
+        const float rpr = 1.0f / (float)pr;
+        for (int e = tid; e < 2 * LR * pr; e += NT) {
+            const int pl = e & 1, rr = e >> 1;
+            const int r = (int)(((float)rr + 0.5f) * rpr), j = rr - r * pr;
+            const int col = j < MPADL / 8 ? 8 * j : W + 8 * j;
+            *reinterpret_cast<h8 *>((pl ? Fl : Fh) + (size_t)r * SB + 2 * col) = h8{};
+        }
+    }
+    int ef;
+    const float sf = pow2_scale(block_max(vm, red), ef);
+#pragma unroll
+    for (int k = 0; k < NV4; ++k) {
+        const int e = tid + k * NT;
+        if (e >= n4) break;
+        const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
+        const float x0 = v[k].x * sf, x1 = v[k].y * sf, x2 = v[k].z * sf, x3 = v[k].w * sf;
+        const h4 hv = {(_Float16)x0, (_Float16)x1, (_Float16)x2, (_Float16)x3};
+        const h4 lv = {(_Float16)(x0 - (float)hv[0]), (_Float16)(x1 - (float)hv[1]),
+                       (_Float16)(x2 - (float)hv[2]), (_Float16)(x3 - (float)hv[3])};
+        const size_t off = (size_t)lr * SB + 2 * (MPADL + 4 * cc);
+        *reinterpret_cast<h4 *>(Fh + off) = hv;
+        *reinterpret_cast<h4 *>(Fl + off) = lv;
+    }
+    __syncthreads();
+
+    const int lane = tid & 63, wave = tid >> 6, l16 = lane & 15, g = lane >> 4;
+    const int tr = wave % TRB;       // tile row of this wave
+    const int tcol0 = wave / TRB;    // tile cols tcol0, tcol0 + WPR, ...
+    const bool row_live = yb0 + tr * 16 < yb1;
+    const size_t plane = (size_t)H * W;
+    float vmax = 0.0f;
+    for (int u = u_beg; u < u_end; ++u) {
+        const tmr_unit_t &un = units[u];
+        const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int roff = __builtin_amdgcn_readfirstlane(un.row_offset);
+        const int et = __builtin_amdgcn_readfirstlane(texp[(size_t)u * a.C + c]);
+        const int ph = h / 2, pw = w / 2, Ho = H - h + 1, Wo = W - w + 1;
+        const int pw_al = (pw + 7) & ~7, s = pw_al - pw;
+        f32x4 acc[NTW];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (row_live) {
+            const char *arow = reinterpret_cast<const char *>(
+                trows + ((int64_t)a.C * roff + (int64_t)c * h) * 2 * TROW + TOFF + 8 * g - l16 - s);
+            const int rb = tr * 16 + l16 + hg - ph;  // LDS row of output row (yb0 + 16 tr + l16) at i = 0
+            if (16 + s + w - 1 <= 32)
+                mfma_unit<NTW, 1, WPR>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+            else
+                mfma_unit<NTW, 2, WPR>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+        }
+        // ---- epilogue: exact unscale, correctly rounded /(h*w), scale, pad mask
+        const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
+        const float denom = (float)(h * w);
+        const float rden = 1.0f / denom;
+        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane : outp + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        const int y = yb0 + tr * 16 + l16;
+        if (row_live && y < yb1) {
+            const bool vy = y >= ph && y < ph + Ho;
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) {
+                const int x = (tcol0 + WPR * t) * 16 + 4 * g;
+                float r4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int xx = x + j;
+                    r4[j] = (vy && xx >= pw && xx < pw + Wo) ? div_cr(acc[t][j] * inv, denom, rden) * sc : 0.0f;
+                    vmax = fmaxf(vmax, fabsf(r4[j]));
+                }
+                *reinterpret_cast<float4 *>(op + (size_t)y * W + x) = float4{r4[0], r4[1], r4[2], r4[3]};
+                if (rp)
+                    *reinterpret_cast<float4 *>(rp + (size_t)y * W + x) =
+                        float4{fmaxf(r4[0], 0.0f), fmaxf(r4[1], 0.0f), fmaxf(r4[2], 0.0f), fmaxf(r4[3], 0.0f)};
+            }
+        }
+    }
+    if (a.out_absmax && !a.squeeze) {
+        const float mx = block_max(vmax, red);
+        if (tid == 0) atomicMax(a.out_absmax + (unsigned)q % TMR_ABSMAX_SLOTS, __float_as_uint(mx));
+    }
+}
+
+// smallest LDS row stride >= bytes with stride = 32 mod 64 (conflict-free B reads)
+static int mfma_row_stride(int bytes) {
+    int sb = (bytes + 63) / 64 * 64 + 32;
+    if (sb - 64 >= bytes) sb -= 64;
+    return sb;
+}
+
 // squeeze (template_matching.py:34-35): sum over channels, pad, scale
 __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_unit_t *__restrict__ units,
                                      int U, int C, int H, int W, const float *__restrict__ scale,
@@ -465,21 +754,96 @@ __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_u
 
 }  // namespace
 
-extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
-                         const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                         int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                         float *work, float *out_absmax, void *stream) {
+// Crossover between the VALU kernels and the MFMA kernel (TMR_XCORR_AUTO):
+// the MFMA kernel runs a launch when every unit's template is at least
+// kMfmaMinK wide or tall (set from the rocprof counters) and
+// the shape fits it (W % 32 == 0, W <= 256, templates <= 31).
+static constexpr int kMfmaMinK = 1;
+
+static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
+    if (W % 32 != 0 || W > 256 || max_ht > 31 || max_wt > 31 || H < 1) return false;
+    const int LR = 32 + 2 * (max_ht / 2);
+    return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
+}
+
+template <int NTW, int NV4, int TRB>
+static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
+                         const _Float16 *trows, const int32_t *texp) {
+    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return TMR_E_HIP;
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB>), dim3(nblk), dim3(NT), lds, s, a, m, trows, texp,
+                       a.out, a.units);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+template <int TRB>
+static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
+                         const _Float16 *trows, const int32_t *texp, int nv4) {
+    const int ntw = a.W / 16 / (4 / TRB);
+    switch (ntw) {
+#define TMR_NTW(K)                                                                       \
+    case K:                                                                              \
+        return nv4 == 8 ? launch_mfma_t<K, 8, TRB>(a, m, lds, nblk, s, trows, texp)      \
+                        : launch_mfma_t<K, 16, TRB>(a, m, lds, nblk, s, trows, texp);
+        TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8)
+#undef TMR_NTW
+        default: return TMR_E_UNSUPPORTED;
+    }
+}
+
+static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, int max_wt,
+                       const void *tmpl_split, int64_t total_rows) {
+    MArgs m;
+    // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
+    // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*)
+    const int trb = 2;
+    m.HG = max_ht / 2;
+    m.HTM = max_ht;
+    m.LR = 16 * trb + 2 * m.HG;
+    const int nk_max = (16 + 7 + max_wt - 1 + 31) / 32;
+    m.SB = mfma_row_stride(2 * (a.W + MPADL + 32 * nk_max));
+    m.nband = (int)tmr_cdiv(a.H, 16 * trb);
+    const int64_t nlog = (int64_t)m.nband * a.C * B;
+    TMR_REQUIRE(nlog < (1LL << 31) - 8);
+    m.nlog = (int)nlog;
+    const size_t lds = 2 * (size_t)m.LR * m.SB + 64;
+    const unsigned nblk = (unsigned)((nlog + 7) / 8 * 8);
+    const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
+    const int32_t *texp = reinterpret_cast<const int32_t *>(trows + (int64_t)a.C * total_rows * 2 * TROW);
+    (void)U;
+    const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
+    return launch_mfma_w<2>(a, m, lds, nblk, s, trows, texp, nv4);
+}
+
+extern "C" int64_t tmr_template_split_size(int U, int C, int64_t total_rows) {
+    if (U <= 0 || C <= 0 || total_rows <= 0) return -1;
+    return (int64_t)C * total_rows * 2 * TROW * 2 + 4 * (int64_t)U * C;
+}
+
+extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
+                                  int64_t total_rows, void *out, void *stream) {
+    TMR_REQUIRE(templates && units && out && U > 0 && C > 0 && total_rows > 0);
+    _Float16 *rows = reinterpret_cast<_Float16 *>(out);
+    int32_t *ex = reinterpret_cast<int32_t *>(rows + (int64_t)C * total_rows * 2 * TROW);
+    const int64_t waves = (int64_t)U * C;
+    hipLaunchKernelGGL(template_split_kernel, dim3((unsigned)tmr_cdiv(waves, 4)), dim3(256), 0,
+                       tmr_stream(stream), templates, units, U, C, total_rows, rows, ex);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
+                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
+                              float *work, float *out_absmax, const void *tmpl_split,
+                              int64_t total_rows, int algo, int min_k, void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
-    // row-tiled kernel when rows are 16-B aligned and templates fit its
-    // width specialisations (template sizes are odd, template_matching.py:66-73)
-    const bool rows = (W % 4) == 0 && max_wt <= 31;
-    const int WS = rows ? W + PADL + PADR : W;
-    // LDS rows: band + template halo + slack rows for partial 4-row tiles
-    const int max_rows = (150 * 1024) / (4 * WS) - 1;
-    const int RB = min(32, max_rows - (max_ht - 1) - (rows ? TRY + 3 : RY));
-    if (RB < 1) return TMR_E_UNSUPPORTED;
+    TMR_REQUIRE(algo >= TMR_XCORR_AUTO && algo <= TMR_XCORR_MFMA);
     XArgs a;
     a.f = f;
     a.tmpl = templates;
@@ -493,24 +857,40 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
     a.C = C;
     a.H = H;
     a.W = W;
-    a.RB = RB;
     a.squeeze = squeeze;
-    a.LR = rows ? RB + max_ht + 3 : RB + max_ht - 1 + RY;
-    a.HG = max_ht / 2;
-    const size_t lds = rows ? (size_t)a.LR * WS * sizeof(float)
-                            : ((size_t)a.LR * W + XSLACK) * sizeof(float);
-    const void *kfn = rows ? (const void *)xcorr_rows_kernel : (const void *)xcorr_kernel;
     hipStream_t s = tmr_stream(stream);
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return TMR_E_HIP;
     TMR_REQUIRE(C < 65536 && B < 65536);
-    dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
-    if (rows)
-        hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
-    else
-        hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
-    TMR_CHECK_LAUNCH();
+    const bool fits = mfma_fits(H, W, max_ht, max_wt) && tmpl_split && total_rows > 0;
+    if (algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
+    const bool use_mfma = algo == TMR_XCORR_MFMA || (algo == TMR_XCORR_AUTO && fits && min_k >= kMfmaMinK);
+    if (use_mfma) {
+        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows);
+        if (rc != TMR_OK) return rc;
+    } else {
+        // row-tiled kernel when rows are 16-B aligned and templates fit its
+        // width specialisations (template sizes are odd, template_matching.py:66-73)
+        const bool rows = (W % 4) == 0 && max_wt <= 31;
+        const int WS = rows ? W + PADL + PADR : W;
+        // LDS rows: band + template halo + slack rows for partial 4-row tiles
+        const int max_rows = (150 * 1024) / (4 * WS) - 1;
+        const int RB = min(32, max_rows - (max_ht - 1) - (rows ? TRY + 3 : RY));
+        if (RB < 1) return TMR_E_UNSUPPORTED;
+        a.RB = RB;
+        a.LR = rows ? RB + max_ht + 3 : RB + max_ht - 1 + RY;
+        a.HG = max_ht / 2;
+        const size_t lds = rows ? (size_t)a.LR * WS * sizeof(float)
+                                : ((size_t)a.LR * W + XSLACK) * sizeof(float);
+        const void *kfn = rows ? (const void *)xcorr_rows_kernel : (const void *)xcorr_kernel;
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return TMR_E_HIP;
+        dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
+        if (rows)
+            hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
+        else
+            hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
+        TMR_CHECK_LAUNCH();
+    }
     if (squeeze) {
         int64_t tot = (int64_t)U * H * W;
         hipLaunchKernelGGL(xcorr_squeeze_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, s,
@@ -519,4 +899,12 @@ extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float
         TMR_CHECK_LAUNCH();
     }
     return TMR_OK;
+}
+
+extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
+                         const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                         int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
+                         float *work, float *out_absmax, void *stream) {
+    return tmr_xcorr_algo(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze,
+                          out, relu_out, work, out_absmax, nullptr, 0, TMR_XCORR_VALU, 1, stream);
 }

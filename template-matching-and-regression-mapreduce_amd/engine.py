@@ -27,8 +27,8 @@ import numpy as np
 import torch
 
 from . import host
-from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_TILED_INIT, SPLIT_TILED_OUT, TMRError,
-                   call, load, ptr, require_gpu, stream)
+from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_TILED_INIT, SPLIT_TILED_OUT, XCORR_ALGOS,
+                   TMRError, call, load, ptr, require_gpu, stream)
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
@@ -58,6 +58,56 @@ class PathConfig:
                    decoder_num_layer=args.decoder_num_layer,
                    decoder_kernel_size=args.decoder_kernel_size, no_matcher=bool(args.no_matcher),
                    precision=getattr(args, "precision", "fp32"))
+
+
+# Correlation-kernel crossover (tmr_xcorr_algo), from the measured launch
+# times of both kernels per template side k (HIP events, kbench_xcorr,
+# profiles/r02c_kbench_xcorr_sweep{128,192}.jsonl), as ms per unit at the
+# 512 x 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
+# exemplars at 128^2; the image's band staging is shared by 3 units) and
+# E = 16 (8 images x 16 exemplars at 192^2, times / 2.25 for the area).
+# "auto" interpolates the regimes in log E, sums the per-unit costs of a
+# launch (linear in k in between) and runs the cheaper kernel: at E = 3 the
+# VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
+# crossover); at E = 16 MFMA wins from k = 9 on.
+XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
+_T128 = {  # ms per 192 units (E = 3), r02c sweep
+    "valu": (1.603, 1.973, 2.488, 3.546, 4.066, 5.758, 6.657, 9.247, 10.356, 14.634, 14.984, 20.271,
+             20.318, 28.515, 27.311, 37.380),
+    "mfma": (2.252, 2.970, 3.653, 4.306, 5.000, 5.683, 6.366, 7.099, 7.832, 14.587, 16.013, 17.468,
+             18.923, 20.383, 21.830, 23.335),
+}
+_K192 = (3, 9, 15, 21, 31)
+_T192 = {  # ms per 128 units (E = 16) at 192^2, r02c sweep
+    "valu": (2.697, 6.027, 14.634, 22.891, 62.326),
+    "mfma": (3.442, 5.849, 8.235, 16.312, 23.813),
+}
+XCORR_COST = {
+    a: (np.asarray(_T128[a]) / 192.0,
+        np.interp(XCORR_COST_K, _K192, np.asarray(_T192[a]) / 128.0 / 2.25))
+    for a in ("valu", "mfma")
+}
+# A mixed-size MFMA launch stages every band with the LARGEST template's halo
+# rows: measured 1.13x the per-k sum at the config-B 3..15 mix (5.57 ms vs
+# 4.91 predicted, profiles/r02b_kbench_xcorr_mixB*); the VALU kernel's mix
+# matches its per-k sum (4.75 vs 4.72).
+XCORR_MFMA_MIX = 1.13
+
+
+def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool) -> str:
+    """The cheaper correlation kernel for a launch over units of these
+    template sizes (XCORR_COST model)."""
+    if not mfma_ok:
+        return "valu"
+    k = np.maximum(np.asarray(ht), np.asarray(wt)).astype(np.float64)
+    lam = float(np.clip(np.log(max(units_per_image, 1.0) / 3.0) / np.log(16.0 / 3.0), 0.0, 1.0))
+    cost = {}
+    for alg, (c3, c16) in XCORR_COST.items():
+        per_k = (1.0 - lam) * c3 + lam * c16
+        cost[alg] = float(np.interp(k, XCORR_COST_K, per_k).sum())
+    if k.size and k.min() != k.max():
+        cost["mfma"] *= XCORR_MFMA_MIX
+    return min(cost, key=cost.get)
 
 
 def _version_key(ts: Sequence[torch.Tensor]):
@@ -272,6 +322,10 @@ class TMREngine:
         # input channels; same linear map, fp32-level rounding differences)
         self.fold_proj = True
         self._absmax_memo: Dict[tuple, tuple] = {}
+        # correlation kernel: "auto" (the crossover rule in tmr_xcorr_algo),
+        # "valu" or "mfma" (csrc/xcorr.hip)
+        self.xcorr_algo = "auto"
+        self.last_xcorr_algo = None
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -475,10 +529,23 @@ class TMREngine:
         if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        call("tmr_xcorr", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh, mw,
-             ptr(scale),
-             int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
-             ptr(work) if work is not None else None, ptr(slots), stream())
+        min_k = int(min(units["ht"].min(), units["wt"].min()))
+        choice = self.xcorr_algo
+        if choice == "auto":  # measured per-k cost model (XCORR_COST)
+            fits = W % 32 == 0 and W <= 256 and mh <= 31 and mw <= 31 and (32 + mh // 2 * 2) * W <= 16384
+            choice = xcorr_choice(units["ht"], units["wt"], U / max(1, len(set(unit_image))), fits)
+        self.last_xcorr_algo = choice
+        algo = XCORR_ALGOS[choice]
+        tsplit = None
+        if algo != XCORR_ALGOS["valu"] and tfl > 0:
+            # hi/lo fp16 operands of the MFMA correlation (per (unit, channel) scale)
+            rows = int(units["ht"].sum())
+            tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
+            call("tmr_template_split", ptr(tmpl), ptr(units_d), U, C, rows, ptr(tsplit), stream())
+        call("tmr_xcorr_algo", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+             mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
+             ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
+             rows if tsplit is not None else 0, algo, min_k, stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)

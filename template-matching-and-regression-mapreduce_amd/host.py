@@ -72,7 +72,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
     U = boxes.shape[0]
     ttype = TEMPLATE_TYPES[template_type]
     units = np.zeros(U, UNIT_DTYPE)
-    off = 0
+    off = rows = 0
     max_ht = max_wt = 1
     for u in range(U):
         units["image"][u] = int(images[u])
@@ -86,7 +86,9 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         units["ht"][u] = ht
         units["wt"][u] = wt
         units["tmpl_offset"][u] = off
+        units["row_offset"][u] = rows
         off += C * ht * wt
+        rows += ht
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
     return units, off, max_ht, max_wt
 

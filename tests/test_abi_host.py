@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_struct_layouts():
-    assert _lib.UNIT_DTYPE.itemsize == 56
+    assert _lib.UNIT_DTYPE.itemsize == 64
     assert _lib.PEAK_DTYPE.itemsize == 24
 
 

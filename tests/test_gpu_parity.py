@@ -553,3 +553,85 @@ def test_reduced_precision_forward_vs_oracle(prec):
         ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]), exm, P)
         assert normwise(o[u], ro[0][0].numpy()) <= SPLIT_TOL[prec]
         assert normwise(b[u], rb[0][0].numpy()) <= SPLIT_TOL[prec]
+
+
+# ----------------------------------------------------------------- xcorr (MFMA)
+@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15), (70, 128, 8, 31),
+                                        (192, 192, 8, 31), (33, 32, 8, 15)])
+def test_xcorr_mfma_vs_oracle(H, W, C, kmax):
+    """The row-Toeplitz MFMA correlation kernel (TMR_XCORR_MFMA, 3-term fp16
+    split) against the C oracle at every odd template side 1..31, rectangular
+    templates, several units per image, band edges (H % 32 != 0), a learned
+    scale, relu output, the fused max |f_TM| and the zero pad border."""
+    from tmr_amd._lib import XCORR_ALGOS, call, ptr, stream
+    from tmr_amd.engine import _h2d, _units_to_device
+    B = 2
+    f = synth.normal(90 + H + W, (B, C, H, W)) * 1.7
+    shapes = [(1, 1), (3, 3), (5, 9), (7, 7), (11, 3), (13, 15), (15, 15), (17, 17), (19, 5), (21, 23),
+              (25, 25), (27, 31), (31, 29), (31, 31), (9, 1), (1, 13)]
+    shapes = [(min(kh, kmax, H // 2 * 2 - 1), min(kw, kmax, W // 2 * 2 - 1)) for kh, kw in shapes]
+    boxes, ui = [], []
+    for u, (kh, kw) in enumerate(shapes):
+        boxes.append(synth.exemplar_box(kh, H, W, (5 * u) % (H - kh + 1), (7 * u) % (W - kw + 1), kw))
+        ui.append(u * B // len(shapes))
+    boxes = np.stack(boxes)
+    units, tfl, mh, mw = host.build_units(boxes, ui, H, W, C)
+    fd = cuda(f)
+    tm = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    tmpl = torch.cat([tm.extract_template(fd[ui[u]:ui[u] + 1], torch.from_numpy(boxes[u])).reshape(-1)
+                      for u in range(len(ui))])
+    ud = _units_to_device(units, DEV)
+    iu = _h2d(host.image_ranges(ui, B), DEV)
+    U = len(ui)
+    scale = torch.tensor([0.75], device=DEV)
+    lib = tmr_amd._lib.load()
+    rows = int(units["ht"].sum())
+    tsplit = torch.empty(lib.tmr_template_split_size(U, C, rows), device=DEV, dtype=torch.uint8)
+    call("tmr_template_split", ptr(tmpl), ptr(ud), U, C, rows, ptr(tsplit), stream())
+    outs = {}
+    for algo in ("valu", "mfma"):
+        out = torch.empty((U, C, H, W), device=DEV)
+        relu = torch.empty_like(out)
+        amax = torch.zeros(256, device=DEV)
+        call("tmr_xcorr_algo", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
+             ptr(out), ptr(relu), None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, stream())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        outs[algo] = got
+        assert amax.max().item() == np.abs(got).max(), algo
+        assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0)), algo
+    tmpl_h = tmpl.cpu().numpy()
+    for u in range(U):
+        ht, wt, off = int(units["ht"][u]), int(units["wt"][u]), int(units["tmpl_offset"][u])
+        t = tmpl_h[off:off + C * ht * wt].reshape(C, ht, wt)
+        ref = oracle.xcorr(f[ui[u]], t, 0.75)
+        for algo, got in outs.items():
+            assert normwise(got[u], ref) <= TOL, (algo, u, ht, wt, normwise(got[u], ref))
+            ph, pw = ht // 2, wt // 2
+            if ph:
+                assert (got[u][:, :ph] == 0).all() and (got[u][:, H - ph:] == 0).all()
+            if pw:
+                assert (got[u][:, :, :pw] == 0).all() and (got[u][:, :, W - pw:] == 0).all()
+
+
+def test_xcorr_mfma_squeeze_and_engine():
+    """squeeze through the MFMA kernel, and TMREngine.match with xcorr_algo
+    'mfma' / 'valu' / 'auto' on the scripted shape (C = 512, 128^2)."""
+    C, H, W = 512, 128, 128
+    f = synth.normal(5, (2, C, H, W))
+    boxes = np.stack([synth.exemplar_box(k, H, W, 10 + k, 3 * k) for k in (3, 9, 15)])
+    ui = [0, 0, 1]
+    res = {}
+    for sq in (False, True):
+        P = {"matcher.scale": torch.tensor([1.25], device=DEV)}
+        for algo in ("valu", "mfma", "auto"):
+            eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C, squeeze=sq))
+            eng.xcorr_algo = algo
+            out, _ = eng.match(cuda(f), ui, boxes)
+            res[(sq, algo)] = out.cpu().numpy()
+        for u in range(3):
+            roi, ht, wt = oracle.template_size(boxes[u], H, W)
+            t = oracle.roi_align(f[ui[u]], roi, ht, wt)
+            ref = oracle.xcorr(f[ui[u]], t, 1.25, sq)
+            for algo in ("valu", "mfma", "auto"):
+                assert normwise(res[(sq, algo)][u], ref) <= TOL, (sq, algo, u)
