@@ -265,19 +265,21 @@ int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U,
  * unit has none (TM_utils.py:288-291).  Unit u's counts[u] candidates start
  * at row unit_off[u] (device int64[U]) of logits [.,2] / box [.,4] /
  * ref [.,2]; the score is logits[.,0] (:319).  seg_units (device int32[G+1]),
- * cand_off (device int64[G+1], the offsets of those unions) and mask_off
- * (device int64[G+1], prefix sums of n_g*ceil(n_g/64)) are computed on the
- * host from the candidate counts (one sync, as the reference's torch.where).
+ * cand_off (device int64[G+1], the offsets of those unions) and nb_off
+ * (device int64[G+1], prefix sums of ceil(n_g/64)) are computed on the
+ * host from the candidate counts (one sync, as the reference's torch.where);
+ * sum_nb = nb_off[G], max_cand = max n_g.
  * Outputs are written per image at cand_off[g]: keep-ordered logits [n,2] =
  * (score, 0), boxes [n,4], refs [n,2], optionally the keep indices (int64,
  * local to the image's union, = torchvision's return value) and kept[g].
- * `work` holds
- * tmr_nms_work_size(total_cand, mask_off[G]) bytes. */
-int64_t tmr_nms_work_size(int64_t total_cand, int64_t mask_words);
+ * Memory is O(total_cand) plus one bounded strip of IoU suppression words
+ * (<= 256 MiB whatever n is): `work` holds
+ * tmr_nms_work_size(total_cand, sum_nb, max_cand, G) bytes. */
+int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G);
 int tmr_nms(const float *logits, const float *box, const float *ref, const int32_t *counts,
             const int64_t *unit_off, const int32_t *seg_units, const int64_t *cand_off,
-            const int64_t *mask_off,
-            int G, int64_t total_cand, int64_t max_cand, double iou_threshold,
+            const int64_t *nb_off,
+            int G, int64_t total_cand, int64_t max_cand, int64_t sum_nb, double iou_threshold,
             float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
             int32_t *kept, void *work, void *stream);
 

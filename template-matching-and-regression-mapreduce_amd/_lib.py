@@ -85,8 +85,8 @@ SIGNATURES = {
     "tmr_split_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
                                   _P, _P, _P, _I, _P]),
     "tmr_peaks_decode": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
-    "tmr_nms_work_size": (_L, [_L, _L]),
-    "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),
+    "tmr_nms_work_size": (_L, [_L, _L, _L, _I]),
+    "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),
     "tmr_feature_stats_work_size": (_L, [_I]),
     "tmr_feature_stats": (_I, [_P, _I, _L, _P, _P, _P]),
 }

@@ -5,40 +5,79 @@
 // Get_pred_boxes results are concatenated (demo.py:123-130,
 // trainer.py:111-118), dummy rows included (TM_utils.py:288-291).
 //
-//   gather : union per image in unit order, dummy row for empty units
-//   rank   : stable descending rank by counting (ties -> lower index)
-//   mask   : upper-triangular 64-bit IoU suppression words per sorted row
-//   reduce : one wave per image walks 64-row blocks; the in-block greedy
-//            chain is resolved from registers (readlane), then the kept rows
-//            are OR-ed into the LDS "removed" bitmap in parallel.  The keep
-//            list equals the sequential torchvision loop because IoU(i,j) is
-//            bitwise symmetric and suppression only flows from kept rows.
+//   gather : union per image in unit order (dummy row for an empty unit)
+//            + the local index of every row
+//   sort   : rocprim segmented radix sort of (score, index) pairs, descending
+//            and stable: ties keep the lower index first, as torchvision's
+//            stable sort (O(n log) per image instead of O(n^2) rank counting)
+//   strips : the 64-bit IoU suppression words of a STRIP of S row blocks
+//            (64 sorted rows each) against every later column block are
+//            computed (mask_strip) and consumed (reduce_strip) strip after
+//            strip.  One wave per image keeps the running "removed" bitmap
+//            (one bit per sorted row, in LDS, parked in HBM between strips):
+//            a block's in-block greedy chain is resolved from registers
+//            (readlane), then its kept rows' words are OR-ed into the later
+//            blocks.  Memory is O(n) per image plus ONE strip buffer whose
+//            size is bounded (TMR_NMS_STRIP_WORDS) independently of n^2; the
+//            keep list equals the sequential torchvision loop because IoU(i,j)
+//            is bitwise symmetric and suppression only flows from kept rows.
 // Built with -ffp-contract=off.
+#include <algorithm>
+
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
 #include "tmr_common.h"
 
 namespace {
 
-constexpr int RANK_NT = 256;
+// strip buffer budget: 32 Mi 64-bit words (256 MiB) across all images of a
+// call; a strip holds S row blocks of every image (S >= 1)
+constexpr int64_t STRIP_WORDS = 32ll << 20;
+// rocprim's temporary storage beyond its key/value double buffers
+constexpr int64_t SORT_SLACK = 1 << 20;
 
 struct NmsWork {
-    float *s;       // [T]
-    float *b;       // [T][4]
-    float *r;       // [T][2]
-    int32_t *order; // [T] sorted position -> local index
-    uint64_t *mask; // [mask_words]
+    float *s;        // [T] scores (unit order)
+    float *skeys;    // [T] sorted scores (unused beyond the sort)
+    float *b;        // [T][4]
+    float *r;        // [T][2]
+    int32_t *idx;    // [T] local row index (sort values in)
+    int32_t *order;  // [T] sorted position -> local index
+    uint64_t *removed;  // [sum_nb] running suppression bitmap per image
+    uint64_t *strip;    // [strip_words]
+    char *temp;         // rocprim temporary storage
+    int64_t temp_bytes;
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-__host__ __device__ inline NmsWork carve(void *work, int64_t T) {
+inline int64_t sort_temp_bound(int64_t T, int G) { return 8 * T + SORT_SLACK + 64 * (int64_t)(G + 1); }
+
+// S (row blocks per strip) and the strip buffer's words for these sizes
+inline void strip_plan(int64_t sum_nb, int64_t max_nb, int64_t &S, int64_t &words) {
+    S = std::max<int64_t>(1, std::min<int64_t>(max_nb, STRIP_WORDS / std::max<int64_t>(1, 64 * sum_nb)));
+    words = S * 64 * sum_nb;
+}
+
+inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int64_t strip_words, int G) {
     NmsWork w;
     char *p = (char *)work;
     w.s = (float *)p; p += align256(sizeof(float) * T);
+    w.skeys = (float *)p; p += align256(sizeof(float) * T);
     w.b = (float *)p; p += align256(sizeof(float) * 4 * T);
     w.r = (float *)p; p += align256(sizeof(float) * 2 * T);
+    w.idx = (int32_t *)p; p += align256(sizeof(int32_t) * T);
     w.order = (int32_t *)p; p += align256(sizeof(int32_t) * T);
-    w.mask = (uint64_t *)p;
+    w.removed = (uint64_t *)p; p += align256(sizeof(uint64_t) * sum_nb);
+    w.strip = (uint64_t *)p; p += align256(sizeof(uint64_t) * strip_words);
+    w.temp = p;
+    w.temp_bytes = sort_temp_bound(T, G);
     return w;
+}
+
+inline int64_t work_bytes(int64_t T, int64_t sum_nb, int64_t strip_words, int G) {
+    const NmsWork w = carve(nullptr, T, sum_nb, strip_words, G);
+    return (int64_t)(w.temp - (char *)nullptr) + w.temp_bytes + 256;
 }
 
 __global__ void gather_kernel(const float *__restrict__ logits, const float *__restrict__ box,
@@ -47,7 +86,8 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
                               const int32_t *__restrict__ seg_units,
                               const int64_t *__restrict__ cand_off, NmsWork w) {
     const int g = blockIdx.x;
-    int64_t pos = cand_off[g];
+    const int64_t off = cand_off[g];
+    int64_t pos = off;
     for (int u = seg_units[g]; u < seg_units[g + 1]; ++u) {
         const int n = counts[u];
         if (n == 0) {
@@ -56,6 +96,7 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
                 w.b[4 * pos + 0] = 0.0f; w.b[4 * pos + 1] = 0.0f;
                 w.b[4 * pos + 2] = 1e-14f; w.b[4 * pos + 3] = 1e-14f;
                 w.r[2 * pos + 0] = 0.0f; w.r[2 * pos + 1] = 0.0f;
+                w.idx[pos] = (int32_t)(pos - off);
             }
             pos += 1;
             continue;
@@ -67,44 +108,24 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
             reinterpret_cast<float4 *>(w.b)[pos + i] = bb;
             w.r[2 * (pos + i) + 0] = ref[2 * (src + i) + 0];
             w.r[2 * (pos + i) + 1] = ref[2 * (src + i) + 1];
+            w.idx[pos + i] = (int32_t)(pos + i - off);
         }
         pos += n;
     }
 }
 
-__global__ __launch_bounds__(RANK_NT) void rank_kernel(const int64_t *__restrict__ cand_off, NmsWork w) {
-    __shared__ float ss[RANK_NT];
-    const int g = blockIdx.y;
-    const int64_t off = cand_off[g];
-    const int n = (int)(cand_off[g + 1] - off);
-    if ((int)blockIdx.x * RANK_NT >= n) return;
-    const int i = blockIdx.x * RANK_NT + threadIdx.x;
-    const float si = i < n ? w.s[off + i] : 0.0f;
-    int rank = 0;
-    for (int j0 = 0; j0 < n; j0 += RANK_NT) {
-        __syncthreads();
-        ss[threadIdx.x] = (j0 + threadIdx.x < n) ? w.s[off + j0 + threadIdx.x] : 0.0f;
-        __syncthreads();
-        const int m = min(RANK_NT, n - j0);
-        for (int k = 0; k < m; ++k) {
-            const float sj = ss[k];
-            const int j = j0 + k;
-            rank += (sj > si) || (sj == si && j < i);
-        }
-    }
-    if (i < n) w.order[off + rank] = i;
-}
-
-__global__ __launch_bounds__(64) void mask_kernel(const int64_t *__restrict__ cand_off,
-                                                  const int64_t *__restrict__ mask_off, double thr,
-                                                  NmsWork w) {
+// IoU words of row block ib = s*S + ibl (64 sorted rows) x column block jb >= ib
+__global__ __launch_bounds__(64) void mask_strip_kernel(const int64_t *__restrict__ cand_off,
+                                                        const int64_t *__restrict__ nb_off, double thr,
+                                                        int64_t S, int64_t s, NmsWork w) {
     __shared__ float jb_box[64][4];
     __shared__ float jb_area[64];
-    const int jb = blockIdx.x, ib = blockIdx.y, g = blockIdx.z;
+    const int jb = blockIdx.x, g = blockIdx.z;
+    const int64_t ib = s * S + blockIdx.y;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
-    if (ib >= nb || jb >= nb || jb < ib) return;
+    if (ib >= nb || jb >= nb || jb < ib) return;  // block-uniform
     const int t = threadIdx.x;
     const int j = jb * 64 + t;
     if (j < n) {
@@ -114,7 +135,7 @@ __global__ __launch_bounds__(64) void mask_kernel(const int64_t *__restrict__ ca
         jb_area[t] = (bj.z - bj.x) * (bj.w - bj.y);
     }
     __syncthreads();
-    const int i = ib * 64 + t;
+    const int i = (int)ib * 64 + t;
     if (i >= n) return;
     const int li = min(max(w.order[off + i], 0), n - 1);
     const float4 bi = reinterpret_cast<const float4 *>(w.b)[off + li];
@@ -132,31 +153,41 @@ __global__ __launch_bounds__(64) void mask_kernel(const int64_t *__restrict__ ca
         const float ovr = inter / (ai + jb_area[k] - inter);
         if ((double)ovr > thr) bits |= (1ull << k);
     }
-    w.mask[mask_off[g] + (int64_t)i * nb + jb] = bits;
+    // strip layout per image: [S*64 rows][nb words]
+    w.strip[S * 64 * nb_off[g] + (int64_t)(blockIdx.y * 64 + t) * nb + jb] = bits;
 }
 
-__global__ __launch_bounds__(64) void reduce_kernel(const int64_t *__restrict__ cand_off,
-                                                    const int64_t *__restrict__ mask_off, NmsWork w,
-                                                    float *__restrict__ out_logits,
-                                                    float *__restrict__ out_boxes,
-                                                    float *__restrict__ out_refs,
-                                                    int64_t *__restrict__ out_keep,
-                                                    int32_t *__restrict__ kept_out) {
+__global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restrict__ cand_off,
+                                                          const int64_t *__restrict__ nb_off, int64_t S,
+                                                          int64_t s, NmsWork w, float *__restrict__ out_logits,
+                                                          float *__restrict__ out_boxes,
+                                                          float *__restrict__ out_refs,
+                                                          int64_t *__restrict__ out_keep,
+                                                          int32_t *__restrict__ kept_out) {
     extern __shared__ uint64_t removed[];
     const int g = blockIdx.x, lane = threadIdx.x;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
-    const uint64_t *mask = w.mask + mask_off[g];
+    const int64_t ib0 = s * S;
+    if (ib0 >= nb) return;  // this image has no rows in the strip
+    uint64_t *grem = w.removed + nb_off[g];
+    const uint64_t *mask = w.strip + S * 64 * nb_off[g];
     for (int k = lane; k < nb; k += 64) {
-        const int rem = n - k * 64;
-        removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
+        if (s == 0) {
+            const int rem = n - k * 64;
+            removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
+        } else {
+            removed[k] = grem[k];
+        }
     }
+    int cnt = s == 0 ? 0 : kept_out[g];
     __syncthreads();
-    int cnt = 0;
-    for (int ib = 0; ib < nb; ++ib) {
+    const int ib1 = (int)std::min<int64_t>(ib0 + S, nb);
+    for (int ib = (int)ib0; ib < ib1; ++ib) {
         const int i = ib * 64 + lane;
-        const uint64_t diag = i < n ? mask[(int64_t)i * nb + ib] : 0ull;
+        const int64_t row = (int64_t)(ib - ib0) * 64;
+        const uint64_t diag = i < n ? mask[(row + lane) * nb + ib] : 0ull;
         uint64_t word = removed[ib];
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
@@ -194,7 +225,7 @@ __global__ __launch_bounds__(64) void reduce_kernel(const int64_t *__restrict__ 
                     if (kb) {
                         const int b = __builtin_ctzll(kb);
                         kb &= kb - 1;
-                        v[t] = mask[(int64_t)(ib * 64 + b) * nb + k];
+                        v[t] = mask[(row + b) * nb + k];
                     }
                 }
                 acc |= ((v[0] | v[1]) | (v[2] | v[3])) | ((v[4] | v[5]) | (v[6] | v[7]));
@@ -203,50 +234,62 @@ __global__ __launch_bounds__(64) void reduce_kernel(const int64_t *__restrict__ 
         }
         __syncthreads();
     }
+    for (int k = lane; k < nb; k += 64) grem[k] = removed[k];
     if (lane == 0) kept_out[g] = cnt;
 }
 
 }  // namespace
 
-extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t mask_words) {
-    if (total_cand < 0 || mask_words < 0) return -1;
-    const int64_t T = total_cand;
-    return (int64_t)(align256(sizeof(float) * T) + align256(sizeof(float) * 4 * T) +
-                     align256(sizeof(float) * 2 * T) + align256(sizeof(int32_t) * T) +
-                     sizeof(uint64_t) * (size_t)mask_words + 256);
+extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
+    if (total_cand < 0 || sum_nb < 0 || max_cand < 0 || G <= 0) return -1;
+    int64_t S, words;
+    strip_plan(sum_nb, (max_cand + 63) / 64, S, words);
+    return work_bytes(total_cand, sum_nb, words, G);
 }
 
 extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
                        const int32_t *counts, const int64_t *unit_off, const int32_t *seg_units,
-                       const int64_t *cand_off, const int64_t *mask_off, int G,
-                       int64_t total_cand, int64_t max_cand, double iou_threshold,
+                       const int64_t *cand_off, const int64_t *nb_off, int G,
+                       int64_t total_cand, int64_t max_cand, int64_t sum_nb, double iou_threshold,
                        float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
                        int32_t *kept, void *work, void *stream) {
-    TMR_REQUIRE(logits && box && ref && counts && unit_off && seg_units && cand_off && mask_off);
+    TMR_REQUIRE(logits && box && ref && counts && unit_off && seg_units && cand_off && nb_off);
     TMR_REQUIRE(work && out_logits && out_boxes && out_refs && kept && G > 0);
-    TMR_REQUIRE(total_cand >= G && max_cand >= 1);
+    TMR_REQUIRE(total_cand >= G && max_cand >= 1 && sum_nb >= G);
+    TMR_REQUIRE(total_cand < (1ll << 31));
     const int64_t max_nb = (max_cand + 63) / 64;
-    TMR_REQUIRE(max_nb < 65536 && G < 65536);
-    TMR_REQUIRE(max_nb * 8 <= 150 * 1024);
+    TMR_REQUIRE(max_nb < (1 << 20) && G < 65536);
+    TMR_REQUIRE(max_nb * 8 <= 150 * 1024);  // the removed bitmap in LDS
     hipStream_t s = tmr_stream(stream);
-    NmsWork w = carve(work, total_cand);
+    int64_t S, strip_words;
+    strip_plan(sum_nb, max_nb, S, strip_words);
+    NmsWork w = carve(work, total_cand, sum_nb, strip_words, G);
     hipLaunchKernelGGL(gather_kernel, dim3(G), dim3(256), 0, s, logits, box, ref, counts, unit_off,
                        seg_units, cand_off, w);
     TMR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rank_kernel, dim3((unsigned)tmr_cdiv(max_cand, RANK_NT), G), dim3(RANK_NT), 0, s,
-                       cand_off, w);
-    TMR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(mask_kernel, dim3((unsigned)max_nb, (unsigned)max_nb, G), dim3(64), 0, s, cand_off,
-                       mask_off, iou_threshold, w);
-    TMR_CHECK_LAUNCH();
+    size_t tb = 0;
+    if (rocprim::segmented_radix_sort_pairs_desc(nullptr, tb, w.s, w.skeys, w.idx, w.order,
+                                                 (unsigned)total_cand, (unsigned)G, cand_off, cand_off + 1,
+                                                 0, 32, s) != hipSuccess)
+        return TMR_E_HIP;
+    if ((int64_t)tb > w.temp_bytes) return TMR_E_INVALID;
+    if (rocprim::segmented_radix_sort_pairs_desc(w.temp, tb, w.s, w.skeys, w.idx, w.order,
+                                                 (unsigned)total_cand, (unsigned)G, cand_off, cand_off + 1,
+                                                 0, 32, s) != hipSuccess)
+        return TMR_E_HIP;
     const size_t lds = sizeof(uint64_t) * (size_t)max_nb;
-    auto rk = reduce_kernel;
+    auto rk = reduce_strip_kernel;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void *)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
         return TMR_E_HIP;
-    hipLaunchKernelGGL(rk, dim3(G), dim3(64), lds, s, cand_off, mask_off, w, out_logits, out_boxes,
-                       out_refs, out_keep, kept);
-    TMR_CHECK_LAUNCH();
+    for (int64_t st = 0; st * S < max_nb; ++st) {
+        hipLaunchKernelGGL(mask_strip_kernel, dim3((unsigned)max_nb, (unsigned)S, G), dim3(64), 0, s, cand_off,
+                           nb_off, iou_threshold, S, st, w);
+        TMR_CHECK_LAUNCH();
+        hipLaunchKernelGGL(rk, dim3(G), dim3(64), lds, s, cand_off, nb_off, S, st, w, out_logits, out_boxes,
+                           out_refs, out_keep, kept);
+        TMR_CHECK_LAUNCH();
+    }
     return TMR_OK;
 }

@@ -744,20 +744,21 @@ class TMREngine:
         (+ keep indices when want_keep)."""
         dev = logits.device
         G = len(seg_units) - 1
-        cand_off, mask_off, max_cand = host.nms_offsets(counts_host, seg_units)
+        cand_off, nb_off, max_cand = host.nms_offsets(counts_host, seg_units)
         T = int(cand_off[-1])
-        work = torch.empty(max(load().tmr_nms_work_size(T, int(mask_off[-1])), 1), device=dev,
+        sum_nb = int(nb_off[-1])
+        work = torch.empty(max(load().tmr_nms_work_size(T, sum_nb, max_cand, G), 1), device=dev,
                            dtype=torch.uint8)
         seg_d = _h2d(np.asarray(seg_units, np.int32), dev)
         coff_d = _h2d(np.asarray(cand_off), dev)
-        moff_d = _h2d(np.asarray(mask_off), dev)
+        nboff_d = _h2d(np.asarray(nb_off), dev)
         out_l = torch.empty((T, 2), device=dev, dtype=torch.float32)
         out_b = torch.empty((T, 4), device=dev, dtype=torch.float32)
         out_r = torch.empty((T, 2), device=dev, dtype=torch.float32)
         kept = torch.empty(G, device=dev, dtype=torch.int32)
         keep = torch.empty(T, device=dev, dtype=torch.int64) if want_keep else None
         call("tmr_nms", ptr(logits), ptr(box), ptr(ref), ptr(counts), ptr(unit_off), ptr(seg_d),
-             ptr(coff_d), ptr(moff_d), G, T, max_cand, float(iou_threshold), ptr(out_l), ptr(out_b),
+             ptr(coff_d), ptr(nboff_d), G, T, max_cand, sum_nb, float(iou_threshold), ptr(out_l), ptr(out_b),
              ptr(out_r), ptr(keep) if keep is not None else None, ptr(kept), ptr(work), stream())
         k = kept.cpu().numpy()  # variable-length result: one sync
         L, Bx, R, K = [], [], [], []

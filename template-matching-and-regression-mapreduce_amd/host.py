@@ -153,7 +153,8 @@ def peak_params(boxes: np.ndarray, H: int, W: int, cls_ths: float, box_reg: bool
 
 def nms_offsets(counts: np.ndarray, seg_units: np.ndarray):
     """Per-image candidate-union sizes (dummy row for an empty unit,
-    TM_utils.py:288-291) -> (cand_off[G+1], mask_off[G+1], max_cand)."""
+    TM_utils.py:288-291) -> (cand_off[G+1], nb_off[G+1], max_cand): nb_off
+    are the prefix sums of ceil(n_g / 64), the 64-row blocks of tmr_nms."""
     counts = np.asarray(counts, np.int64)
     G = len(seg_units) - 1
     n = np.zeros(G, np.int64)
@@ -162,7 +163,6 @@ def nms_offsets(counts: np.ndarray, seg_units: np.ndarray):
         n[g] = int(np.maximum(c, 1).sum())
     cand_off = np.zeros(G + 1, np.int64)
     cand_off[1:] = np.cumsum(n)
-    words = n * ((n + 63) // 64)
-    mask_off = np.zeros(G + 1, np.int64)
-    mask_off[1:] = np.cumsum(words)
-    return cand_off, mask_off, int(n.max()) if G else 0
+    nb_off = np.zeros(G + 1, np.int64)
+    nb_off[1:] = np.cumsum((n + 63) // 64)
+    return cand_off, nb_off, int(n.max()) if G else 0

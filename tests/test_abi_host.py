@@ -44,7 +44,10 @@ def test_size_queries_no_gpu():
     assert L.tmr_conv_pack_size(512, 256, 1) == 4 * 8 * 32 * 128
     assert L.tmr_conv_pack_size(10, 10, 4) == -1
     assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
-    assert L.tmr_nms_work_size(10, 4) > 10 * 36
+    assert L.tmr_nms_work_size(10, 4, 5, 3) > 10 * 40
+    # bounded: the IoU words of 64 images x 49,152 candidates stay within the strip budget
+    big = L.tmr_nms_work_size(64 * 49152, 64 * 768, 49152, 64)
+    assert big < 64 * 49152 * 64 + (300 << 20)
 
 
 def test_split_size_queries_no_gpu():
@@ -68,7 +71,7 @@ def test_invalid_arguments_return_codes():
     assert L.tmr_conv_pack(None, 1, 1, 3, None, None) == -1
     assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None,
                        None) == -1
-    assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0.5, *([None] * 7)) == -1
+    assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0, 0.5, *([None] * 7)) == -1
     # split conv: bad precision / kernel size / missing scale sources never launch
     assert L.tmr_split_conv_store(None, 0, None, None, 8, 1, 8, 8, 3, 9, None, None, None, None, 8, 0,
                                   None, None, 0, None) == -1
@@ -157,10 +160,10 @@ def test_adaptive_kernel_api():
 def test_nms_offsets_dummy_rule():
     counts = np.array([3, 0, 5, 0, 0, 2])
     seg = np.array([0, 3, 6])
-    cand_off, mask_off, mx = host.nms_offsets(counts, seg)
+    cand_off, nb_off, mx = host.nms_offsets(counts, seg)
     assert cand_off.tolist() == [0, 9, 13]  # 3+1+5, 1+1+2
     assert mx == 9
-    assert mask_off.tolist() == [0, 9, 13]  # n*ceil(n/64)
+    assert nb_off.tolist() == [0, 1, 2]  # prefix sums of ceil(n/64)
 
 
 def test_state_dict_keys_match_reference(golden):

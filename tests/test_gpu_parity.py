@@ -635,3 +635,38 @@ def test_xcorr_mfma_squeeze_and_engine():
             ref = oracle.xcorr(f[ui[u]], t, 1.25, sq)
             for algo in ("valu", "mfma", "auto"):
                 assert normwise(res[(sq, algo)][u], ref) <= TOL, (sq, algo, u)
+
+
+def test_nms_worst_case_dense_candidates():
+    """SURVEY.md §7.3.3 worst case: a centre-only adaptive kernel (exemplars
+    under 2 px) with p ~ 0.5 everywhere at cls 0.1 makes EVERY pixel a
+    candidate: n = E * H * W = 49,152 per image (E = 3, 128^2), two images.
+    Boxes decoded from wide regressions overlap heavily.  The strip NMS
+    (bounded memory, sorted by a segmented radix sort) keeps exactly the
+    oracle's sequential torchvision list."""
+    H = W = 128
+    B, E = 2, 3
+    U = B * E
+    o = synth.normal(501, (U, 1, H, W)) * 0.05  # p = sigmoid(o) ~ 0.5, near-ties
+    o[:, :, ::7, ::5] = 0.0  # exact ties across units
+    reg = synth.normal(502, (U, 4, H, W)) * 0.4
+    reg[:, 2:] += 2.3  # exp -> ~10x the exemplar size: dense overlaps
+    boxes = np.array([[0.3, 0.3, 0.3 + 1.5 / W, 0.3 + 1.5 / H]] * U, np.float32)
+    params = host.peak_params(boxes, H, W, 0.1)
+    assert (params["mask"] == host.KERNEL_CENTER).all()
+    logits, box, ref, counts, prob = tmr_amd.TMREngine.peaks(cuda(o), cuda(reg), params)
+    counts_h = counts.cpu().numpy()
+    assert (counts_h == H * W).all()
+    unit_off = torch.arange(U, device=DEV, dtype=torch.int64) * (H * W)
+    L, Bx, R, K = tmr_amd.TMREngine.nms(logits, box, ref, counts, counts_h, unit_off,
+                                         np.arange(0, U + 1, E), 0.5, want_keep=True)
+    lg = logits.cpu().numpy().reshape(U, H * W, 2)
+    bx = box.cpu().numpy().reshape(U, H * W, 4)
+    for img in range(B):
+        cb = bx[img * E:(img + 1) * E].reshape(-1, 4)
+        cs = lg[img * E:(img + 1) * E, :, 0].reshape(-1)
+        keep = oracle.nms(cb, cs, 0.5)
+        assert cb.shape[0] == 49152
+        assert np.array_equal(K[img].cpu().numpy(), keep), img
+        assert bits_equal(Bx[img].cpu().numpy(), cb[keep])
+        assert bits_equal(L[img].cpu().numpy()[:, 0], cs[keep])
