@@ -83,6 +83,12 @@ int tmr_upsample_proj(const float *feat, int B, int Cin, int Hin, int Win, int u
                       const float *wpack, const float *bias, int N, float *fp, float *f0,
                       void *stream);
 
+/* f[0] = F.interpolate(feat, scale_factor=2, mode='bilinear',
+ * align_corners=False) alone (matching_net.py:50-51, the API output :81):
+ * feat [BC][Hin][Win] -> out [BC][2 Hin][2 Win], bit-exact with ATen's CPU
+ * kernel's fma nesting. */
+int tmr_upsample2x(const float *feat, int BC, int Hin, int Win, float *out, void *stream);
+
 /* ---- (a6+a7+a8) exemplar templates --------------------------------------
  * torchvision.ops.roi_align(f, [roi], (ht,wt), aligned=True) per unit
  * (models/template_matching.py:75) or the prototype AdaptiveAvgPool2d(1)

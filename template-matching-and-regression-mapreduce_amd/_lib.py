@@ -58,6 +58,7 @@ SIGNATURES = {
     "tmr_conv_pack_size": (_L, [_I, _I, _I]),
     "tmr_conv_pack": (_I, [_P, _I, _I, _I, _P, _P]),
     "tmr_upsample_proj": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P]),
+    "tmr_upsample2x": (_I, [_P, _I, _I, _I, _P, _P]),
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
     "tmr_xcorr_algo": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,

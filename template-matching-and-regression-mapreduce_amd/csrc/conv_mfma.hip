@@ -383,6 +383,15 @@ extern "C" int tmr_conv_pack(const float *w, int N, int C, int ks, float *wpack,
     return TMR_OK;
 }
 
+extern "C" int tmr_upsample2x(const float *feat, int BC, int Hin, int Win, float *out, void *stream) {
+    TMR_REQUIRE(feat && out && BC > 0 && Hin > 0 && Win > 0);
+    const int64_t tot = (int64_t)BC * 4 * Hin * Win;
+    hipLaunchKernelGGL(upsample2x_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, tmr_stream(stream),
+                       feat, BC, Hin, Win, out);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
 extern "C" int tmr_upsample_proj(const float *feat, int B, int Cin, int Hin, int Win, int upsample,
                                  const float *wpack, const float *bias, int N, float *fp,
                                  float *f0, void *stream) {

@@ -1,10 +1,12 @@
 // Exemplar templates (gfx950): RoIAlign (torchvision 0.19 semantics, as
 // called at models/template_matching.py:75 with aligned=True,
 // sampling_ratio=-1, spatial_scale=1) and the prototype average
-// (template_matching.py:43-53).  One workgroup per unit; the sampling grid is
-// computed once per unit into LDS and reused by every channel, like
-// torchvision's CPU pre_calc.  Built with -ffp-contract=off: every product and
+// (template_matching.py:43-53).  Workgroups per (unit, channel group); the
+// sampling grid is computed once per workgroup into LDS and reused by every
+// channel, like torchvision's CPU pre_calc.  Built with -ffp-contract=off: every product and
 // sum is a separately rounded fp32 op, as in the reference's CPU kernel.
+#include <algorithm>
+
 #include "tmr_common.h"
 
 namespace {
@@ -63,7 +65,9 @@ __global__ __launch_bounds__(NT) void roi_align_kernel(const float *__restrict__
     const float *fb = f + (size_t)un.image * C * H * W;
     float *out = tmpl + un.tmpl_offset;
     const int per_c = PH * PW;
-    for (int e = threadIdx.x; e < C * per_c; e += NT) {
+    // this block's channel range (grid.y splits the unit's channels)
+    const int c0 = (int)((int64_t)C * blockIdx.y / gridDim.y), c1 = (int)((int64_t)C * (blockIdx.y + 1) / gridDim.y);
+    for (int e = c0 * per_c + threadIdx.x; e < c1 * per_c; e += NT) {
         const int c = e / per_c, q0 = (e % per_c) * g;
         const float *fc = fb + (size_t)c * H * W;
         float acc = 0.0f;
@@ -104,7 +108,10 @@ extern "C" int tmr_templates(const float *f, int B, int C, int H, int W, const t
     TMR_REQUIRE(f && units && templates && B > 0 && C > 0 && H > 0 && W > 0 && U > 0);
     TMR_REQUIRE(max_ht > 0 && max_wt > 0);
     hipStream_t s = tmr_stream(stream);
-    hipLaunchKernelGGL(roi_align_kernel, dim3(U), dim3(NT), 0, s, f, C, H, W, units, templates);
+    // channel groups per unit: enough workgroups for the chip at small U
+    // (the module API runs one unit per call), >= 8 channels each
+    const int cg = (int)std::max<int64_t>(1, std::min<int64_t>(C / 8, tmr_cdiv(1024, U)));
+    hipLaunchKernelGGL(roi_align_kernel, dim3(U, cg), dim3(NT), 0, s, f, C, H, W, units, templates);
     TMR_CHECK_LAUNCH();
     hipLaunchKernelGGL(prototype_kernel, dim3(U, (unsigned)tmr_cdiv(C, NT / 64) > 64 ? 64 : (unsigned)tmr_cdiv(C, NT / 64)),
                        dim3(NT), 0, s, f, C, H, W, units, templates);

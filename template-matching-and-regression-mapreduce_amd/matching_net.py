@@ -74,6 +74,10 @@ class matching_net(nn.Module):
         P = self.path_params()
         if self._engine is None:
             self._engine = TMREngine(P, PathConfig.from_args(self.args))
+            # the callers run one forward per exemplar on the same features
+            # (demo.py:111, trainer.py:96): reuse the image's projection and
+            # decoder fp half across those calls (same values, fp32 contract)
+            self._engine.reuse_image_work = True
         else:
             self._engine.P = P
         return self._engine

@@ -262,3 +262,33 @@ def test_trainer_each_step_call_forms():
                                         args.NMS_cls_threshold, args.NMS_iou_threshold)
     assert bits_equal(pl[0].cpu().numpy(), gl) and bits_equal(pb[0].cpu().numpy(), gb)
     assert bits_equal(prf[0].cpu().numpy(), gr)
+
+
+def test_module_reuse_follows_inputs_and_weights():
+    """The module API keeps an image's projection and decoder fp half across
+    its per-exemplar calls: results still follow a NEW feature tensor, an
+    in-place feature update and in-place weight updates (optimizer steps)."""
+    args, model, P, feats, ex = _model_and_inputs(seed=31, B=1, E=2)
+    fd = cuda(feats)
+    exm = [cuda(ex[0, :1])]
+
+    def check(f_host, label):
+        Pc = {k: v.detach().cpu() for k, v in model.path_params().items()}
+        with torch.no_grad():
+            po, pr, _, _ = model(fd if f_host is feats else cuda(f_host), exm)
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(f_host), [torch.from_numpy(ex[0, :1])], Pc)
+        assert normwise(po[0].cpu().numpy(), ro[0].numpy()) <= TOL, label
+        assert normwise(pr[0].cpu().numpy(), rb[0].numpy()) <= TOL, label
+
+    check(feats, "first call")
+    check(feats, "memo hit")
+    with torch.no_grad():
+        model.input_proj[0].weight.mul_(1.03)
+    check(feats, "input_proj updated")
+    with torch.no_grad():
+        model.decoder_o.layer[0].weight.mul_(0.97)
+    check(feats, "decoder updated")
+    with torch.no_grad():
+        fd.mul_(1.1)
+    check(feats * np.float32(1.1), "features updated in place")
+    check(synth.sam_features(99, 1, feats.shape[1], feats.shape[2], feats.shape[3]), "new tensor")
