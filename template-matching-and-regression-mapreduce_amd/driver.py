@@ -60,25 +60,32 @@ def pack_rows(logits: Sequence[torch.Tensor], boxes: Sequence[torch.Tensor],
 def all_gather_detections(counts: torch.Tensor, rows: torch.Tensor, group=None):
     """The reducer's exchange step.  Every rank receives, in global image
     order, the per-image counts and the concatenated detection rows.
-    Three all-gathers: image counts per rank, per-image counts (padded to the
-    largest rank), rows (padded to the largest rank total)."""
+
+    Two all-gathers: the (images, rows) sizes of every rank, then ONE payload
+    per rank -- its per-image counts (int32 bit patterns in a float32 column
+    block) followed by its rows, padded to the largest rank's payload.  The
+    one host sync between them sizes the payload (the counts are data
+    dependent, like the reference's torch.where sync).  At config B each rank
+    sends 64 counts + ~105 k rows x 28 B ~ 2.9 MB per step (23 MB received per
+    rank at 8 GPUs)."""
     world = dist.get_world_size(group)
     dev = rows.device
     nimg = torch.tensor([counts.numel(), rows.shape[0]], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(nimg) for _ in range(world)]
     dist.all_gather(sizes, nimg, group=group)
     sizes = torch.stack(sizes).cpu().numpy()
-    bmax, rmax = int(sizes[:, 0].max()), int(sizes[:, 1].max())
-    cpad = torch.zeros(max(bmax, 1), dtype=torch.int32, device=dev)
-    cpad[:counts.numel()] = counts
-    call = [torch.zeros_like(cpad) for _ in range(world)]
-    dist.all_gather(call, cpad, group=group)
-    rpad = torch.zeros((max(rmax, 1), ROW), dtype=torch.float32, device=dev)
-    rpad[:rows.shape[0]] = rows
-    rall = [torch.zeros_like(rpad) for _ in range(world)]
-    dist.all_gather(rall, rpad, group=group)
-    g_counts = torch.cat([call[r][:int(sizes[r, 0])] for r in range(world)])
-    g_rows = torch.cat([rall[r][:int(sizes[r, 1])] for r in range(world)])
+    # payload rows: ceil(images / ROW) rows of counts, then the detection rows
+    crow = -(-sizes[:, 0] // ROW)
+    pmax = int((crow + sizes[:, 1]).max())
+    pad = torch.zeros((max(pmax, 1), ROW), dtype=torch.float32, device=dev)
+    nc = int(-(-counts.numel() // ROW))
+    if counts.numel():
+        pad.view(-1)[:counts.numel()] = counts.to(torch.int32).view(torch.float32)
+    pad[nc:nc + rows.shape[0]] = rows
+    got = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(got, pad, group=group)
+    g_counts = torch.cat([got[r].view(-1)[:int(sizes[r, 0])].view(torch.int32) for r in range(world)])
+    g_rows = torch.cat([got[r][int(crow[r]):int(crow[r]) + int(sizes[r, 1])] for r in range(world)])
     return g_counts, g_rows
 
 
