@@ -259,10 +259,15 @@ int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image, con
  * p >= thr, row-major compaction (no cap), decode.  Outputs per unit u at
  * stride cap = H*W: logits[(u*cap+i)*2] = (p, 0) (TM_utils.py:260-261),
  * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u].
- * prob [U,H,W] receives the probability map (required). */
+ * prob [U,H,W] receives the probability map (required).
+ * exp_table (device, nullable): the reference-exp table (tmr_amd/exp_table.py:
+ * 128-B header, uint32 offsets[65537], sorted uint16 low halves).  The decode's
+ * exp (TM_utils.py:272) is the correctly rounded value except at the table's
+ * inputs, where it is the other neighbour, as the reference's torch.exp (MKL
+ * vsExp) rounds; NULL = correctly rounded everywhere. */
 int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H, int W,
                      const tmr_peak_param_t *params, float *prob, float *logits, float *box,
-                     float *ref, int32_t *counts, void *stream);
+                     float *ref, int32_t *counts, const void *exp_table, void *stream);
 
 /* ---- (a17-a19) per-image greedy NMS over the exemplar-ordered union --------
  * torchvision.ops.nms (utils/TM_utils.py:317-323) on, per image g, the

@@ -9,6 +9,10 @@
 //      (torch.where order, no cap), and the candidate is decoded in place:
 //      ref = (x/W, y/H); xy = ref + r[:2]*s; wh = exp(r[2:])*(bw,bh);
 //      box = (xy - wh/2, xy + wh/2).
+// exp: the reference's torch.exp (ATen CPU -> MKL VML vsExp, high accuracy)
+// restated as the correctly rounded value except at the inputs recorded in
+// the reference-exp table (tmr_amd/exp_table.py), where MKL rounds to the
+// other neighbour; without a table, correctly rounded.
 // Built with -ffp-contract=off so every op is separately rounded as in the
 // reference's elementwise torch ops.
 #include "tmr_common.h"
@@ -16,6 +20,29 @@
 namespace {
 
 constexpr int NT = 1024;
+constexpr int EXP_HEADER = 128;  // tmr_amd/exp_table.py
+
+struct ExpTable {
+    const uint32_t *off;  // [65537] by the input's upper 16 bits
+    const uint16_t *lo;   // sorted lower 16 bits of the recorded inputs
+};
+
+__device__ __forceinline__ float expf_ref(float x, ExpTable t) {
+    const double e = exp((double)x);
+    float y = (float)e;
+    if (!t.off) return y;
+    const uint32_t b = __float_as_uint(x);
+    const uint32_t hb = b >> 16, key = b & 0xffffu;
+    uint32_t s = t.off[hb], n = t.off[hb + 1];
+    const uint32_t end = n;
+    while (s < n) {  // lower bound of key in lo[s, end)
+        const uint32_t m = (s + n) >> 1;
+        if (t.lo[m] < key) s = m + 1; else n = m;
+    }
+    if (s < end && t.lo[s] == key)  // MKL rounded to the exact value's other side
+        y = e > (double)y ? nextafterf(y, __builtin_inff()) : nextafterf(y, -__builtin_inff());
+    return y;
+}
 
 __global__ void prob_kernel(const float *__restrict__ o, int64_t n, int is_prob,
                             float *__restrict__ p) {
@@ -47,7 +74,8 @@ __global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ pro
                                                    const float *__restrict__ reg, int H, int W,
                                                    const tmr_peak_param_t *__restrict__ params,
                                                    float *__restrict__ logits, float *__restrict__ box,
-                                                   float *__restrict__ ref, int32_t *__restrict__ counts) {
+                                                   float *__restrict__ ref, int32_t *__restrict__ counts,
+                                                   ExpTable et) {
     __shared__ int wsum[NT / 64];
     const int u = blockIdx.x;
     const tmr_peak_param_t pp = params[u];
@@ -90,7 +118,7 @@ __global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ pro
         }
         const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
         const float cx = rx + r0 * sx, cy = ry + r1 * sy;
-        const float w = tmr_expf_cr(r2) * pp.scale_w, h = tmr_expf_cr(r3) * pp.scale_h;
+        const float w = expf_ref(r2, et) * pp.scale_w, h = expf_ref(r3, et) * pp.scale_h;
         const float hw2 = w / 2.0f, hh2 = h / 2.0f;
         logits[2 * k + 0] = v;
         logits[2 * k + 1] = 0.0f;
@@ -107,15 +135,22 @@ __global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ pro
 
 extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H,
                                 int W, const tmr_peak_param_t *params, float *prob, float *logits,
-                                float *box, float *ref, int32_t *counts, void *stream) {
+                                float *box, float *ref, int32_t *counts, const void *exp_table,
+                                void *stream) {
     TMR_REQUIRE(o && params && prob && logits && box && ref && counts && U > 0 && H > 0 && W > 0);
     hipStream_t s = tmr_stream(stream);
+    ExpTable et = {nullptr, nullptr};
+    if (exp_table) {
+        const char *base = reinterpret_cast<const char *>(exp_table);
+        et.off = reinterpret_cast<const uint32_t *>(base + EXP_HEADER);
+        et.lo = reinterpret_cast<const uint16_t *>(base + EXP_HEADER + 4 * 65537);
+    }
     int64_t n = (int64_t)U * H * W;
     hipLaunchKernelGGL(prob_kernel, dim3((unsigned)tmr_cdiv(n, 256)), dim3(256), 0, s, o, n,
                        input_is_prob, prob);
     TMR_CHECK_LAUNCH();
     hipLaunchKernelGGL(peaks_kernel, dim3(U), dim3(NT), 0, s, prob, reg, H, W, params, logits, box, ref,
-                       counts);
+                       counts, et);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

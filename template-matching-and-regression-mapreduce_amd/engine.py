@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from . import host
+from . import exp_table, host
 from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_TILED_INIT, SPLIT_TILED_OUT, XCORR_ALGOS,
                    TMRError, call, load, ptr, require_gpu, stream)
 
@@ -765,6 +765,11 @@ class TMREngine:
         return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
 
     # ------------------------------------------------------------ post
+    # the decode's exp (TM_utils.py:272): "reference" = the reference's
+    # torch.exp (MKL vsExp) through the recorded table (exp_table.py),
+    # "cr" = correctly rounded
+    exp_mode = "reference"
+
     @staticmethod
     def peaks(o: torch.Tensor, b: Optional[torch.Tensor], params: np.ndarray,
               input_is_prob: bool = False):
@@ -783,8 +788,10 @@ class TMREngine:
         ref = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         counts = torch.empty(U, device=dev, dtype=torch.int32)
         bb = b.float().contiguous() if b is not None else None
+        tab = exp_table.device_table(dev) if TMREngine.exp_mode == "reference" else None
         call("tmr_peaks_decode", ptr(o), int(input_is_prob), ptr(bb) if bb is not None else None,
-             U, H, W, ptr(prm), ptr(prob), ptr(logits), ptr(box), ptr(ref), ptr(counts), stream())
+             U, H, W, ptr(prm), ptr(prob), ptr(logits), ptr(box), ptr(ref), ptr(counts),
+             ptr(tab) if tab is not None else None, stream())
         return logits, box, ref, counts, prob
 
     @staticmethod
