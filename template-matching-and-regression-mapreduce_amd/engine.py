@@ -88,10 +88,13 @@ XCORR_COST = {
     for a in ("valu", "mfma")
 }
 # A mixed-size MFMA launch stages every band with the LARGEST template's halo
-# rows: measured 1.13x the per-k sum at the config-B 3..15 mix (5.57 ms vs
-# 4.91 predicted, profiles/r02b_kbench_xcorr_mixB*); the VALU kernel's mix
-# matches its per-k sum (4.75 vs 4.72).
-XCORR_MFMA_MIX = 1.13
+# rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
+# units when an image has few of them: measured 1.13x the per-k sum at the
+# config-B 3..15 mix with 3 units per image (5.57 ms vs 4.91,
+# profiles/r02b_kbench_xcorr_mixB*), 1.46x for the k >= 11 units of that batch
+# (~2 per image; profiles/r02c_bench_B* by_class); the VALU kernel's mixes match
+# its per-k sums (4.75 vs 4.72).  Empirical: 1 + 0.4 / units-per-image.
+XCORR_MFMA_MIX = 0.4
 
 
 def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool) -> str:
@@ -106,7 +109,7 @@ def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok
         per_k = (1.0 - lam) * c3 + lam * c16
         cost[alg] = float(np.interp(k, XCORR_COST_K, per_k).sum())
     if k.size and k.min() != k.max():
-        cost["mfma"] *= XCORR_MFMA_MIX
+        cost["mfma"] *= 1.0 + XCORR_MFMA_MIX / max(units_per_image, 1.0)
     return min(cost, key=cost.get)
 
 
