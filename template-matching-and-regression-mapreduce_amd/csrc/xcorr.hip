@@ -30,6 +30,7 @@
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;
 constexpr int RY = 2;  // output rows per lane
@@ -277,13 +278,22 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
     constexpr int NV = (OFF + KW + TRX + 3) / 4;   // b128 reads per row (+1 float for odd pairs)
     constexpr int NO = (OFF + KW + TRX - 2) / 2;   // odd pairs (x[2m+1], x[2m+2])
     for (int ii = 0; ii < TRY + h - 1; ++ii) {
-        const float4 *xr = reinterpret_cast<const float4 *>(xs + (lrow0 + ii) * WS + lcol0);
+        const f32x4 *xr = reinterpret_cast<const f32x4 *>(xs + (lrow0 + ii) * WS + lcol0);
         f32x2 xe[2 * NV], xo[NO];
+        f32x4 v4[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v4[j] = xr[j];
+        // Pin every window vector whole in 4 consecutive VGPRs: left alone,
+        // the compiler narrows the partly used vectors into ds_read2_b32 /
+        // ds_read2_b64 of the odd-aligned pairs (4- / 2-way bank conflicts
+        // at a 16-B lane stride, and ~1 v_mov per FMA to rebuild the even
+        // pairs) -- the xcorr kernel's SQ_LDS_BANK_CONFLICT of round 1.
+#pragma unroll
+        for (int j = 0; j < NV; ++j) asm volatile("" : "+v"(v4[j]));
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            const float4 v4 = xr[j];
-            xe[2 * j] = f32x2{v4.x, v4.y};
-            xe[2 * j + 1] = f32x2{v4.z, v4.w};
+            xe[2 * j] = f32x2{v4[j].x, v4[j].y};
+            xe[2 * j + 1] = f32x2{v4[j].z, v4[j].w};
         }
 #pragma unroll
         for (int m = 0; m < NO; ++m) xo[m] = f32x2{xe[m].y, xe[m + 1].x};
@@ -468,7 +478,6 @@ constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct MArgs {
     int SB;     // LDS plane row stride in bytes (32 mod 64)
