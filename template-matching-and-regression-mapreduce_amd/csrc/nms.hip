@@ -13,11 +13,11 @@
 //   strips : the 64-bit IoU suppression words of a STRIP of S row blocks
 //            (64 sorted rows each) against every later column block are
 //            computed (mask_strip) and consumed (reduce_strip) strip after
-//            strip.  One wave per image keeps the running "removed" bitmap
-//            (one bit per sorted row, in LDS, parked in HBM between strips):
-//            a block's in-block greedy chain is resolved from registers
-//            (readlane), then its kept rows' words are OR-ed into the later
-//            blocks.  Memory is O(n) per image plus ONE strip buffer whose
+//            strip.  One workgroup per image keeps the running "removed"
+//            bitmap (one bit per sorted row, in LDS, parked in HBM between
+//            strips): a row block's in-block greedy chain is resolved from
+//            registers (readlane over the surviving rows), then its kept
+//            rows' words are OR-ed into the later blocks by all its threads.  Memory is O(n) per image plus ONE strip buffer whose
 //            size is bounded (TMR_NMS_STRIP_WORDS) independently of n^2; the
 //            keep list equals the sequential torchvision loop because IoU(i,j)
 //            is bitwise symmetric and suppression only flows from kept rows.
@@ -157,7 +157,15 @@ __global__ __launch_bounds__(64) void mask_strip_kernel(const int64_t *__restric
     w.strip[S * 64 * nb_off[g] + (int64_t)(blockIdx.y * 64 + t) * nb + jb] = bits;
 }
 
-__global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restrict__ cand_off,
+// One block of RT threads per image.  Every wave resolves the block's greedy
+// chain itself (the same 64 diagonal words and the same removed word, so the
+// same kept mask, with no barrier to broadcast it); wave 0 writes the kept
+// rows; the OR of the kept rows' words into the later column blocks -- the
+// bulk of the work, (nb - ib) words per kept row -- is spread over all RT
+// threads (one wave per image left 8 waves running chip-wide at config E).
+constexpr int RT = 256;
+
+__global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restrict__ cand_off,
                                                           const int64_t *__restrict__ nb_off, int64_t S,
                                                           int64_t s, NmsWork w, float *__restrict__ out_logits,
                                                           float *__restrict__ out_boxes,
@@ -165,15 +173,16 @@ __global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restr
                                                           int64_t *__restrict__ out_keep,
                                                           int32_t *__restrict__ kept_out) {
     extern __shared__ uint64_t removed[];
-    const int g = blockIdx.x, lane = threadIdx.x;
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const bool w0 = tid < 64;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
     const int64_t ib0 = s * S;
-    if (ib0 >= nb) return;  // this image has no rows in the strip
+    if (ib0 >= nb) return;  // this image has no rows in the strip (block-uniform)
     uint64_t *grem = w.removed + nb_off[g];
     const uint64_t *mask = w.strip + S * 64 * nb_off[g];
-    for (int k = lane; k < nb; k += 64) {
+    for (int k = tid; k < nb; k += RT) {
         if (s == 0) {
             const int rem = n - k * 64;
             removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
@@ -191,14 +200,17 @@ __global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restr
         uint64_t word = removed[ib];
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
-        for (int bit = 0; bit < 64; ++bit) {
-            if ((word >> bit) & 1ull) continue;
+        // walk the surviving rows only (lowest first): each kept row's
+        // diagonal word suppresses later rows of the block
+        for (uint64_t avail = ~word; avail;) {
+            const int bit = __builtin_ctzll(avail);
             kept |= 1ull << bit;
             const uint32_t lo = __builtin_amdgcn_readlane(dlo, bit);
             const uint32_t hi = __builtin_amdgcn_readlane(dhi, bit);
             word |= ((uint64_t)hi << 32) | lo;
+            avail = bit == 63 ? 0ull : ~word & (~0ull << (bit + 1));
         }
-        if ((kept >> lane) & 1ull) {
+        if (w0 && ((kept >> lane) & 1ull)) {
             const int pos = cnt + __popcll(kept & ((1ull << lane) - 1));
             const int li = min(max(w.order[off + i], 0), n - 1);
             const int64_t src = off + li, dst = off + pos;
@@ -210,11 +222,11 @@ __global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restr
             if (out_keep) out_keep[dst] = li;
         }
         cnt += __popcll(kept);
-        // OR the kept rows' words into the later blocks: lane k gathers
-        // column block k (coalesced across lanes); the kept rows (a
-        // wave-uniform set) are walked 8 at a time so 8 independent loads are
-        // in flight per wait instead of one load latency per kept row
-        for (int k = ib + 1 + lane; k < nb; k += 64) {
+        // OR the kept rows' words into the later blocks: thread t gathers
+        // column block ib+1+t (coalesced across lanes); the kept rows (a
+        // block-uniform set) are walked 8 at a time so 8 independent loads
+        // are in flight per wait instead of one load latency per kept row
+        for (int k = ib + 1 + tid; k < nb; k += RT) {
             uint64_t acc = 0;
             uint64_t kb = kept;
             while (kb) {
@@ -234,8 +246,8 @@ __global__ __launch_bounds__(64) void reduce_strip_kernel(const int64_t *__restr
         }
         __syncthreads();
     }
-    for (int k = lane; k < nb; k += 64) grem[k] = removed[k];
-    if (lane == 0) kept_out[g] = cnt;
+    for (int k = tid; k < nb; k += RT) grem[k] = removed[k];
+    if (tid == 0) kept_out[g] = cnt;
 }
 
 }  // namespace
@@ -287,7 +299,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
         hipLaunchKernelGGL(mask_strip_kernel, dim3((unsigned)max_nb, (unsigned)S, G), dim3(64), 0, s, cand_off,
                            nb_off, iou_threshold, S, st, w);
         TMR_CHECK_LAUNCH();
-        hipLaunchKernelGGL(rk, dim3(G), dim3(64), lds, s, cand_off, nb_off, S, st, w, out_logits, out_boxes,
+        hipLaunchKernelGGL(rk, dim3(G), dim3(RT), lds, s, cand_off, nb_off, S, st, w, out_logits, out_boxes,
                            out_refs, out_keep, kept);
         TMR_CHECK_LAUNCH();
     }
