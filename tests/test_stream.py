@@ -265,3 +265,158 @@ def test_stream_cli_on_feature_tree(tmp_path, capsys):
         assert got[4] == exp[4] and got[2] == exp[2] and got[3] == exp[3]  # count, max, sparsity exact
         np.testing.assert_allclose(got[:2], exp[:2], rtol=1e-6, atol=1e-6)
     assert out.splitlines()[0].startswith("CATEGORY")
+
+
+# ---------------------------------------------------------------- backbone producer (§8f f3)
+def _png_bytes(arr, mode):
+    from PIL import Image
+    buf = __import__("io").BytesIO()
+    Image.fromarray(arr, mode).save(buf, format="PNG")
+    return buf.getvalue()
+
+
+def _jpeg_bytes(arr):
+    from PIL import Image
+    buf = __import__("io").BytesIO()
+    Image.fromarray(arr, "RGB").save(buf, format="JPEG", quality=90)
+    return buf.getvalue()
+
+
+def _tar_tree(root, shards, seed=7):
+    """Tar shards as the reference's Gen_Tar_Data ones: images at any depth,
+    mixed formats/modes/case, plus a non-image and an undecodable .png."""
+    import io
+    import tarfile
+    rng = np.random.default_rng(seed)
+    os.makedirs(root, exist_ok=True)
+    n_ok = []
+    for si, name in enumerate(shards):
+        members = []
+        k = int(rng.integers(0, 4))
+        for j in range(k):
+            h, w = int(rng.integers(20, 90)), int(rng.integers(20, 90))
+            kind = (si + j) % 4
+            if kind == 0:
+                members.append((f"img_{j}.png", _png_bytes(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), "RGB")))
+            elif kind == 1:
+                members.append((f"sub/dir/IMG_{j}.PNG", _png_bytes(rng.integers(0, 256, (h, w), dtype=np.uint8), "L")))
+            elif kind == 2:
+                members.append((f"a/img_{j}.jpeg", _jpeg_bytes(rng.integers(0, 256, (h, w, 3), dtype=np.uint8))))
+            else:
+                members.append((f"img_{j}.Jpg", _png_bytes(rng.integers(0, 256, (h, w, 4), dtype=np.uint8), "RGBA")))
+        members.append(("notes.txt", b"not an image"))
+        if si % 3 == 0:
+            members.append(("broken.png", b"\x89PNG garbage"))
+        with tarfile.open(os.path.join(root, name), "w") as tf:
+            for mname, data in members:
+                ti = tarfile.TarInfo(mname)
+                ti.size = len(data)
+                tf.addfile(ti, io.BytesIO(data))
+        n_ok.append(k)
+    return n_ok
+
+
+class _PoolBackbone(torch.nn.Module):
+    """A small deterministic stand-in encoder: 16x16 average pooling + a fixed
+    1x1 projection to C channels (the real SAM encoder is registered the same way)."""
+
+    def __init__(self, C=8):
+        super().__init__()
+        g = torch.Generator().manual_seed(5)
+        self.proj = torch.nn.Conv2d(3, C, 1)
+        with torch.no_grad():
+            self.proj.weight.copy_(torch.randn(C, 3, 1, 1, generator=g))
+            self.proj.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        self.num_channels = C
+
+    def forward(self, x):
+        return self.proj(torch.nn.functional.avg_pool2d(x, 16))
+
+
+def test_tar_images_and_preprocess(tmp_path):
+    """mapper.py:22-32 + :85-88: image members at any depth, extension test
+    case-insensitive, non-images ignored, undecodable images dropped; the
+    preprocessing is PIL RGB -> resize (PIL's default filter, bicubic in the
+    Pillow of this image and of the reference's pinned environment) -> /255
+    -> [1,3,H,W] float32.  Parity unpinned beyond PIL itself (onnxruntime, which
+    the reference mapper imports at module load, is absent here)."""
+    from PIL import Image
+    shards = ["Easy_0.tar", "Hard_1.tar", "Normal_2.tar", "Easy_3.tar"]
+    n_ok = _tar_tree(str(tmp_path), shards)
+    for si, name in enumerate(shards):
+        names = [m for m, _ in mr.tar_images(str(tmp_path / name))]
+        assert names == sorted(names)
+        assert "notes.txt" not in names
+        assert len(names) == n_ok[si] + (1 if si % 3 == 0 else 0)
+    src = mr.TarImageSource(str(tmp_path), shards, _PoolBackbone(), torch.device("cpu"), 2, 3, 5, 0,
+                            input_shape=(64, 48))
+    assert src.counts == n_ok
+    for i in range(len(src.items)):
+        path, member, _ = src.items[i]
+        x = src._read(i)
+        assert x.shape == (1, 3, 48, 64) and x.dtype == np.float32
+        import tarfile
+        with tarfile.open(path) as tf:
+            img = Image.open(tf.extractfile(member)).convert("RGB")
+        ref = np.asarray(img.resize((64, 48), Image.Resampling.BICUBIC)).astype(np.float32) / np.float32(255.0)
+        np.testing.assert_array_equal(x[0], ref.transpose(2, 0, 1))
+    assert mr.preprocess_image(b"garbage") is None
+
+
+def test_tar_source_feature_cache_roundtrip(tmp_path):
+    """The producer's features, written as the mapper's .npy cache, read back
+    by NpyFeatureSource: same files/layout, bit-identical features and
+    per-tar records (CPU stats)."""
+    shards = [f"{c}_{i}.tar" for c in ("Normal", "Easy", "Hard") for i in range(3)]
+    _tar_tree(str(tmp_path / "tars"), shards, seed=11)
+    bb = _PoolBackbone().eval()
+    src = mr.TarImageSource(str(tmp_path / "tars"), shards, bb, torch.device("cpu"), 2, 3, 5, 0,
+                            write_root=str(tmp_path / "feat"), workers=2, input_shape=(128, 128))
+    rec = mr.run_mapper(shards, src.counts, 0, 1, src, _cpu_stats, None, batch=3)
+    src.flush()
+    back = mr.NpyFeatureSource(str(tmp_path / "feat"), shards, torch.device("cpu"), 2, 3, 5, 0)
+    assert back.counts == src.counts
+    assert sorted(back.keys) == sorted(src.keys)
+    for i, key in enumerate(src.keys):
+        j = back.keys.index(key)
+        f_back, _ = back([j])
+        with torch.no_grad():
+            f_new = bb(torch.from_numpy(src._read(i)))
+        assert f_back.shape == (1, 8, 8, 8)
+        assert torch.equal(f_back, f_new)
+    rec2 = mr.run_mapper(shards, back.counts, 0, 1, back, _cpu_stats, None, batch=3)
+    # same per-tar sums up to the image order inside a tar (sorted member
+    # paths vs sorted file stems)
+    np.testing.assert_allclose(rec2, rec, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_stream_cli_tar_producer(tmp_path, capsys):
+    """stream.py main() over tar shards through a registered backbone on the
+    GPU, writing the feature cache; a second run over that cache gives the
+    same mapper lines (the stats kernel on identical features)."""
+    from tmr_amd import register_backbone, unregister_backbone
+    shards = [f"{c}_{i}.tar" for c in ("Normal", "Easy", "Hard") for i in range(3)]
+    _tar_tree(str(tmp_path / "tars"), shards, seed=13)
+    register_backbone("test_pool", lambda args: _PoolBackbone(C=32))
+    try:
+        lst = tmp_path / "list.txt"
+        lst.write_text("".join(s + "\n" for s in shards))
+        common = ["--list", str(lst), "--exemplars", "2", "--kmax", "5", "--stats-only"]
+        mr.main(common + ["--tars-root", str(tmp_path / "tars"), "--backbone", "test_pool",
+                          "--write-features", str(tmp_path / "feat"), "--mapper-out", str(tmp_path / "a.txt")])
+        out_a = capsys.readouterr().out
+        mr.main(common + ["--features-root", str(tmp_path / "feat"), "--mapper-out", str(tmp_path / "b.txt")])
+        out_b = capsys.readouterr().out
+    finally:
+        unregister_backbone("test_pool")
+    a = open(str(tmp_path / "a.txt")).read().splitlines()
+    b = open(str(tmp_path / "b.txt")).read().splitlines()
+    assert len(a) == len(b) > 0
+    for la, lb in zip(a, b):
+        assert la.split("\t")[0] == lb.split("\t")[0]
+        va = [float(v) for v in la.split("\t")[1].split(",")]
+        vb = [float(v) for v in lb.split("\t")[1].split(",")]
+        assert va[4] == vb[4]
+        np.testing.assert_allclose(va, vb, rtol=1e-12)
+    assert out_a.splitlines()[0].startswith("CATEGORY") and out_a == out_b
