@@ -1,4 +1,4 @@
-# r02i: VALU correlation kernel with whole-b128 window reads (old vs new), parity
+# r02i: VALU correlation kernel variants (old = previous build, new = this tree), parity
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

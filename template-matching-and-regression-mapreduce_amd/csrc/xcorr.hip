@@ -270,6 +270,14 @@ constexpr int PADL = 20;  // >= 15 + 3 (max half-width + OFF), multiple of 4
 constexpr int PADR = 24;  // covers the window over-read past column W
 constexpr int TRY = 4;  // max tile rows (the LDS slack rows cover it)
 
+// (a.y, b.x) as ONE v_pk_mov_b32 (left to itself the compiler often builds
+// the odd pair with two v_mov_b32)
+__device__ __forceinline__ f32x2 odd_pair(f32x2 a, f32x2 b) {
+    f32x2 r;
+    asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int KW, int TRY, int TRX>
 __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, int lcol0,
                                           const float *__restrict__ tc, int h,
@@ -296,7 +304,7 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
             xe[2 * j + 1] = f32x2{v4[j].z, v4[j].w};
         }
 #pragma unroll
-        for (int m = 0; m < NO; ++m) xo[m] = f32x2{xe[m].y, xe[m + 1].x};
+        for (int m = 0; m < NO; ++m) xo[m] = odd_pair(xe[m], xe[m + 1]);
 #pragma unroll
         for (int r = 0; r < TRY; ++r) {
             const int i = ii - r;
