@@ -205,8 +205,6 @@ def main():
         model = tmr.build_model(margs)
         model.load_state_dict(P, strict=True)
         model = model.to(dev).eval()
-        ex_d = torch.from_numpy(ex).to(dev)
-        per_image = [[[ex_d[b, e].unsqueeze(0)] for e in range(E)] for b in range(B)]  # demo.py:106
         dummy = {"regression_ablation_b": False, "regression_ablation_c": False}
 
         def step():
@@ -214,8 +212,11 @@ def main():
             with torch.no_grad():
                 for b in range(B):
                     image = feats_d[b:b + 1]
+                    # the image's exemplar boxes arrive with it, as from the
+                    # reference's loader (fresh device tensors every image)
+                    ex_d = torch.from_numpy(ex[b]).to(dev)
                     pl, pb, pr = [], [], []
-                    for exemplar in per_image[b]:
+                    for exemplar in [[ex_d[e].unsqueeze(0)] for e in range(E)]:  # demo.py:106
                         po, preg, _, _ = model(image, exemplar)
                         _l, _b, _r = tmr.Get_pred_boxes(po, preg, exemplar, dummy, cfg["cls"], True)
                         pl.append(_l[0]); pb.append(_b[0]); pr.append(_r[0])

@@ -12,6 +12,8 @@ epilogue (one rounding of the product, as ``f * self.scale``).
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 from torch import nn
@@ -21,9 +23,26 @@ from ._lib import UNIT_DTYPE, TMRError, call, ptr, require_gpu, stream
 from .engine import PathConfig, TMREngine, _h2d, _units_to_device
 
 
+# Host copies of exemplar tensors, keyed on the tensor object (weak
+# reference), its storage and its version: the callers pass the SAME exemplar
+# tensor to matching_net.forward and then to Get_pred_boxes (demo.py:111-112,
+# trainer.py:96-97), and the second device->host read would wait for the whole
+# forward to drain before the host can queue the decode.
+_BOX_MEMO: "dict[int, tuple]" = {}
+
+
 def _box_host(exemplar_coord) -> np.ndarray:
     if isinstance(exemplar_coord, torch.Tensor):
-        return exemplar_coord.detach().float().cpu().numpy().reshape(4)
+        t = exemplar_coord
+        key = id(t)
+        hit = _BOX_MEMO.get(key)
+        if hit is not None and hit[0]() is t and hit[1] == (t._version, t.data_ptr()):
+            return hit[2].copy()
+        v = t.detach().float().cpu().numpy().reshape(4)
+        if len(_BOX_MEMO) > 4096:
+            _BOX_MEMO.clear()
+        _BOX_MEMO[key] = (weakref.ref(t), (t._version, t.data_ptr()), v.copy())
+        return v
     return np.asarray(exemplar_coord, np.float32).reshape(4)
 
 

@@ -12,7 +12,7 @@ import torch
 
 from . import host
 from ._lib import TMRError, require_gpu
-from .engine import TMREngine
+from .engine import TMREngine, _h2d
 from .template_matching import _box_host
 
 
@@ -89,9 +89,9 @@ def _nms_lists(pred_logits, pred_boxes, ref_points, iou_threshold, want_keep=Fal
         counts_h = ns[live]
         unit_off = np.zeros(len(live), np.int64)
         unit_off[1:] = np.cumsum(counts_h)[:-1]
-        counts = torch.as_tensor(counts_h.astype(np.int32), device=dev)
+        counts = _h2d(counts_h.astype(np.int32), dev)  # staged, no stream sync
         seg = np.arange(len(live) + 1, dtype=np.int64)
-        r = TMREngine.nms(lg, bx, rf, counts, counts_h, torch.as_tensor(unit_off, device=dev), seg,
+        r = TMREngine.nms(lg, bx, rf, counts, counts_h, _h2d(unit_off, dev), seg,
                           iou_threshold, want_keep=want_keep)
         for i, g in enumerate(live):
             outs[g] = tuple(x[i] for x in r)
