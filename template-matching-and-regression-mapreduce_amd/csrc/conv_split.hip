@@ -56,6 +56,17 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// Register-staged operand loads (Geo::wcount: buffer_load_dwordx4 to VGPRs,
+// ds_write_b128 a step later, two steps of lookahead) instead of LDS-DMA.
+// Correct (the GPU parity suite passes with it) but measured slower at config
+// B: heads 29.93 vs 28.86 ms per 48 units, 427 vs 436 images/s
+// (profiles/r02p_*) -- the ds_write data transfer and the lgkmcnt waits it
+// adds to the fragment reads cost more than the LDS-DMA issue it saves.
+#ifndef TMR_SPLIT_RS
+#define TMR_SPLIT_RS 0
+#endif
 
 constexpr int BM = 128;      // output channels per block
 constexpr int TH = 16;       // output rows per block
@@ -234,6 +245,22 @@ struct Geo {
         }
         return n;
     }
+    // Register-staged operand path (RS; D == 1 geometries with SPC >= 2): the
+    // weights of step g+2 are loaded into VGPRs during step g and written to
+    // LDS during step g+1 (into the buffer step g read), so an LDS buffer pair
+    // gives two steps of load latency; the next half-chunk's halo is loaded
+    // during steps 0..SPC-2 and written one step later.  A buffer_load +
+    // ds_write_b128 pair issues in a fraction of an LDS-DMA's cost.
+    static constexpr int wcount(int sgx, int part, int halves) {  // pieces per wave, step sg+x
+        return (T - (sgx % SPC) * TPS < TPS ? T - (sgx % SPC) * TPS : TPS) * ipt(lo_of(sgx, part, halves)) /
+               NWAVES;
+    }
+    static constexpr int QL = SPC >= 2 ? (MPW + SPC - 2) / (SPC - 1) : MPW;  // halo loads per step
+    static constexpr int hl(int sg) {
+        return sg > SPC - 2 ? 0 : MPW - sg * QL < QL ? (MPW - sg * QL > 0 ? MPW - sg * QL : 0) : QL;
+    }
+    static constexpr int hs(int sg) { return sg == 0 ? 0 : hl(sg - 1); }
+    static constexpr int MAXW = TPS * NPLW * 2 / NWAVES;  // weight pieces per wave of a hi step
     static_assert(fits(TPS, NWB), "LDS");
 };
 
@@ -321,6 +348,15 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         char *dst = Hs + (hc & 1) * HB;
         buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + (wave + NWAVES * m) * 1024), hoff(m), soff);
     };
+    // the same piece through a VGPR quad (RS path): load, and write to LDS later
+    auto halo_load = [&](int hc, int m) -> v4u {
+        const bool s0 = hc < h0;
+        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;
+        return __builtin_amdgcn_raw_buffer_load_b128(s0 ? xr0 : xr1, hoff(m), soff, 0);
+    };
+    auto halo_store = [&](int hc, int m, v4u v) {
+        *reinterpret_cast<v4u *>(Hs + (hc & 1) * HB + (wave + NWAVES * m) * 1024 + lane * 16) = v;
+    };
     // weights of flat step g: half-chunk g / SPC (hi: wh and wl planes, lo:
     // wh only), taps TPS*(g % SPC)...; instruction i of the step = tap i/IPT,
     // plane (i%IPT)/2, channels 64*((i%IPT)&1) + lane: 1 KB contiguous in the
@@ -334,15 +370,27 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // the caller knows at compile time: ipt instructions per tap, every wave
     // issuing the same count (ipt is a multiple of NWAVES).  g == S (past the
     // end) loads harmless in-range bytes into the free buffer.
-    auto w_dma1 = [&](int g, int ipt, int m) {
+    auto w_src = [&](int g, int ipt, int m) -> uint32_t {
         const int hc = g / SPC, t0 = (g - hc * SPC) * TPS;
         const int c = hc / HALVES;
         const uint32_t src = (uint32_t)t0 * tapstride + (uint32_t)c * a.Npad * WREC + wnt;
-        char *dst = Ws + (g % NWB) * WB;
         const int i = wave + NWAVES * m;
         const int tl = i / ipt, wi = i - tl * ipt;
-        const uint32_t so = src + (uint32_t)tl * tapstride + (uint32_t)(wi >> 1) * a.Npad * 16 + (wi & 1) * 64 * 16;
-        buffer_lds16(wr, (lds_ptr_t)(dst + tl * WB1 + wi * 1024), wlane, so);
+        return src + (uint32_t)tl * tapstride + (uint32_t)(wi >> 1) * a.Npad * 16 + (wi & 1) * 64 * 16;
+    };
+    auto w_dst = [&](int g, int ipt, int m) -> char * {
+        const int i = wave + NWAVES * m;
+        const int tl = i / ipt, wi = i - tl * ipt;
+        return Ws + (g % NWB) * WB + tl * WB1 + wi * 1024;
+    };
+    auto w_dma1 = [&](int g, int ipt, int m) {
+        buffer_lds16(wr, (lds_ptr_t)w_dst(g, ipt, m), wlane, w_src(g, ipt, m));
+    };
+    auto w_load = [&](int g, int ipt, int m) -> v4u {
+        return __builtin_amdgcn_raw_buffer_load_b128(wr, wlane, w_src(g, ipt, m), 0);
+    };
+    auto w_store = [&](int g, int ipt, int m, v4u v) {
+        *reinterpret_cast<v4u *>(w_dst(g, ipt, m) + lane * 16) = v;
     };
 
     // accumulators start at acc_init (scaled into the accumulator's units by
@@ -404,7 +452,17 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
         for (int m = 0; m < nt0; ++m) w_dma1(g0, ipt_of(lo0), m);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    constexpr bool RS = TMR_SPLIT_RS && D == 1 && SPC >= 2;
+    v4u rw[G::MAXW > 0 ? G::MAXW : 1], rh[G::QL > 0 ? G::QL : 1];  // RS: pieces in flight
+    if constexpr (RS) {
+        // the weights of step 1 into VGPRs (step 0 writes them to LDS)
+        constexpr int n1 = G::wcount(1, 0, HALVES);
+#pragma unroll
+        for (int m = 0; m < n1; ++m) rw[m] = w_load(1, ipt_of(G::lo_of(1, 0, HALVES)), m);
+        wait_vmcnt(n1);  // the DMAs above (older) have landed
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
         // one half-chunk; PART is a compile-time constant (F16X3: 0 = hi, 1 = lo)
@@ -427,12 +485,31 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 constexpr int nh = G::nh(sg);
                 constexpr bool loD = G::lo_of(sg + D, part, HALVES);
                 constexpr int nw = G::nw(sg, part, HALVES);
-                auto dma_slot = [&](int k) {  // DMA k of this step (k < nh + nw)
-                    if (k < nh)
-                        halo_dma1(hc + 1, sg * Q + k);
-                    else
-                        w_dma1(g + D, ipt_of(loD), k - nh);
+                // RS: first write the pieces loaded during the previous step
+                // (halo slice of hc+1, weights of g+1), then load the next
+                // ones (halo slice, weights of g+2) into the freed VGPRs
+                constexpr int nsh = RS ? G::hs(sg) : 0, nsw = RS ? G::wcount(sg + 1, part, HALVES) : 0;
+                constexpr int nlh = RS ? G::hl(sg) : 0, nlw = RS ? G::wcount(sg + 2, part, HALVES) : 0;
+                constexpr bool lo1 = G::lo_of(sg + 1, part, HALVES), lo2 = G::lo_of(sg + 2, part, HALVES);
+                constexpr int NSLOT = RS ? nsh + nsw + nlh + nlw : nh + nw;
+                auto dma_slot = [&](int k) {  // slot k of this step (k < NSLOT)
+                    if constexpr (RS) {
+                        if (k < nsh)
+                            halo_store(hc + 1, (sg - 1) * G::QL + k, rh[k]);
+                        else if (k < nsh + nsw)
+                            w_store(g + 1, ipt_of(lo1), k - nsh, rw[k - nsh]);
+                        else if (k < nsh + nsw + nlh)
+                            rh[k - nsh - nsw] = halo_load(hc + 1, sg * G::QL + (k - nsh - nsw));
+                        else
+                            rw[k - nsh - nsw - nlh] = w_load(g + 2, ipt_of(lo2), k - nsh - nsw - nlh);
+                    } else {
+                        if (k < nh)
+                            halo_dma1(hc + 1, sg * Q + k);
+                        else
+                            w_dma1(g + D, ipt_of(loD), k - nh);
+                    }
                 };
+                auto slot_kind = [&](int k) { return RS && k < nsh + nsw ? 0x200 : 0x020; };  // DS write / VMEM
                 const char *wl = Ws + (g % NWB) * WB;
                 // Register pipeline: the A (weight) fragments of a tap are
                 // read during the previous tap of the step, the B (halo)
@@ -479,7 +556,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                             if (j < na) aw[(tl + 1) & 1][jp * APG + j] = afrag(tl + 1, jp * APG + j);
                         // DMA slot k = q - 1 (groups 1.. of the step)
                         const int k = q - 1;
-                        const bool dm = k >= 0 && k < nh + nw;
+                        const bool dm = k >= 0 && k < NSLOT;
                         if (dm) dma_slot(k);
                         const V b = bx[q % NB];
 #pragma unroll
@@ -492,7 +569,12 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                         else if (nr == 1)
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                        if (dm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                        if (dm) {
+                            if (slot_kind(k) == 0x200)
+                                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                            else
+                                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                        }
                         __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     }
                 }
@@ -500,12 +582,15 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 // built here, kept for safety)
 #pragma unroll
                 for (int k = 0; k < 16; ++k)
-                    if (k >= ntap * 8 - 1 && k < nh + nw) dma_slot(k);
+                    if (k >= ntap * 8 - 1 && k < NSLOT) dma_slot(k);
                 __builtin_amdgcn_sched_barrier(0);
                 // the next step needs W(g+1) and, after a half-chunk's last
-                // step, the whole halo of hc+1: leave only younger DMAs in
-                // flight (in-order completion; halo issued before weights)
-                if (D == 1)
+                // step, the whole halo of hc+1: RS -- this step's LDS writes
+                // done; DMA -- leave only younger DMAs in flight (in-order
+                // completion; halo issued before weights)
+                if constexpr (RS)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                else if (D == 1)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 else
                     wait_vmcnt(G::allowed(sg, part, HALVES));
