@@ -253,6 +253,14 @@ int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image, con
                          int leaky, const float *headw, const float *acc_init,
                          float *partials, int flags, void *stream);
 
+/* ---- (a16) custom_shape_3x3_maxpool2d -----------------------------------
+ * utils/TM_utils.py:337-361 on device fp32 planes x [planes][H][W]: out[e] =
+ * the max over the 3x3 neighbourhood taps selected by mask9 (bit 3*r + c is
+ * kernel[r][c]; zero padding as F.unfold), taps in row-major order, a NaN
+ * propagates and ties keep the earlier tap.  mask9 == 0 (an empty selection,
+ * which torch.max rejects) or bits above 8 return TMR_E_INVALID. */
+int tmr_maxpool3x3(const float *x, int64_t planes, int H, int W, int mask9, float *out, void *stream);
+
 /* ---- (a14-a16) peak finder + box decode ------------------------------------
  * Get_pred_boxes per unit (utils/TM_utils.py:245-282): p = sigmoid(o) (or o
  * itself when input_is_prob), masked 3x3 local max with zero padding,

@@ -13,11 +13,13 @@ from .matching_net import Backbone_Encoder, build_encoder, build_model, matching
 from .regression_head import BboxesHead, Decoder_model, ObjectnessHead  # noqa: F401
 from .template_matching import TemplateMatching  # noqa: F401
 from .tm_utils import (NMS, Get_pred_boxes, Make_Template_size_predictions,  # noqa: F401
-                       NMS_process, adaptive_kernel_generater)
+                       NMS_process, adaptive_kernel_generater, calc_area, custom_shape_3x3_maxpool2d,
+                       map_normalization)
 
 __all__ = [
     "TemplateMatching", "Decoder_model", "ObjectnessHead", "BboxesHead", "matching_net",
     "build_model", "Backbone_Encoder", "build_encoder", "Get_pred_boxes", "NMS", "NMS_process",
-    "adaptive_kernel_generater", "Make_Template_size_predictions", "TMREngine", "PathConfig",
+    "adaptive_kernel_generater", "Make_Template_size_predictions", "custom_shape_3x3_maxpool2d",
+    "calc_area", "map_normalization", "TMREngine", "PathConfig",
     "TMRError", "build_backbone", "register_backbone", "unregister_backbone", "FeatureInput",
 ]

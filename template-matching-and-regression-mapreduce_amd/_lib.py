@@ -86,6 +86,7 @@ SIGNATURES = {
     "tmr_split_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I,
                                   _P, _P, _P, _I, _P]),
     "tmr_peaks_decode": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tmr_maxpool3x3": (_I, [_P, _L, _I, _I, _I, _P, _P]),
     "tmr_nms_work_size": (_L, [_L, _L, _L, _I]),
     "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),
     "tmr_feature_stats_work_size": (_L, [_I]),

@@ -52,6 +52,31 @@ __global__ void prob_kernel(const float *__restrict__ o, int64_t n, int is_prob,
     p[i] = is_prob ? v : tmr_sigmoid_cr(v);
 }
 
+// custom_shape_3x3_maxpool2d (TM_utils.py:337-361): per element, the max of
+// the masked 3x3 neighbourhood (F.unfold's zero padding), taps in row-major
+// order; a NaN propagates (torch.max) and a tie keeps the earlier tap.
+__global__ void maxpool3x3_kernel(const float *__restrict__ x, int64_t n, int H, int W, int mask,
+                                  float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t hw = (int64_t)H * W;
+    const int64_t pl = i / hw;
+    const int r = (int)(i - pl * hw), y = r / W, xx = r % W;
+    const float *p = x + pl * hw;
+    float mx = 0.0f;
+    bool first = true;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            if (!((mask >> ((dy + 1) * 3 + dx + 1)) & 1)) continue;
+            const int yy = y + dy, xc = xx + dx;
+            const float q = (yy < 0 || yy >= H || xc < 0 || xc >= W) ? 0.0f : p[yy * W + xc];
+            if (first || q > mx || (q != q && mx == mx)) { mx = q; first = false; }
+        }
+    out[i] = mx;
+}
+
 __device__ __forceinline__ bool is_peak(const float *__restrict__ p, int H, int W, int y, int x,
                                         int mask, float thr) {
     const float v = p[y * W + x];
@@ -132,6 +157,18 @@ __global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ pro
 }
 
 }  // namespace
+
+extern "C" int tmr_maxpool3x3(const float *x, int64_t planes, int H, int W, int mask9, float *out,
+                              void *stream) {
+    if (planes < 0 || H < 0 || W < 0 || (mask9 & 0x1ff) == 0 || (mask9 & ~0x1ff) != 0) return TMR_E_INVALID;
+    const int64_t n = planes * H * W;
+    if (n == 0) return TMR_OK;
+    if (!x || !out) return TMR_E_INVALID;
+    hipLaunchKernelGGL(maxpool3x3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       x, n, H, W, mask9, out);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
 
 extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H,
                                 int W, const tmr_peak_param_t *params, float *prob, float *logits,

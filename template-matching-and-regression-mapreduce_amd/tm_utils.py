@@ -1,4 +1,4 @@
-"""Drop-in post-processing (reference: utils/TM_utils.py:13-18, 224-377).
+"""Drop-in post-processing (reference: utils/TM_utils.py:9-18, 224-377).
 
 ``Get_pred_boxes`` and ``NMS`` keep the reference's signatures, argument
 conventions and list-of-per-image-tensors results; the peak finder, decode
@@ -11,9 +11,43 @@ import numpy as np
 import torch
 
 from . import host
-from ._lib import TMRError, require_gpu
+from ._lib import TMRError, call, ptr, require_gpu, stream
 from .engine import TMREngine, _h2d
 from .template_matching import _box_host
+
+
+def calc_area(box):
+    """TM_utils.py:9-11."""
+    x1, y1, x2, y2 = box
+    return (x2 - x1) * (y2 - y1)
+
+
+def map_normalization(img):
+    """TM_utils.py:325-335: min-max scaling of a map (display helper; torch
+    ops on the tensor's own device, numpy for arrays, as the reference)."""
+    if torch.is_tensor(img):
+        maxv, minv = torch.max(img), torch.min(img)
+    else:
+        maxv, minv = np.max(img), np.min(img)
+    return (img - minv) / (maxv - minv + 1e-14)
+
+
+def custom_shape_3x3_maxpool2d(x: torch.Tensor, kernel: list) -> torch.Tensor:
+    """TM_utils.py:337-361 on the GPU (tmr_maxpool3x3): the max over the
+    3x3 neighbourhood positions where ``kernel`` is 1 (zero padding, as
+    F.unfold), [N,C,H,W] -> [N,C,H,W] in x's dtype (the max is exact)."""
+    require_gpu(x, "x")
+    if x.dim() != 4:
+        raise TMRError(f"custom_shape_3x3_maxpool2d: expected [N,C,H,W], got {tuple(x.shape)}")
+    k = np.asarray(kernel, dtype=bool).reshape(3, 3)
+    mask = int(sum(1 << (3 * r + c) for r in range(3) for c in range(3) if k[r, c]))
+    if mask == 0:  # torch.max over an empty selection raises too
+        raise TMRError("custom_shape_3x3_maxpool2d: the kernel selects no position")
+    xf = x.detach().float().contiguous()
+    N, C, H, W = xf.shape
+    out = torch.empty_like(xf)
+    call("tmr_maxpool3x3", ptr(xf), N * C, H, W, mask, ptr(out), stream())
+    return out if x.dtype == torch.float32 else out.to(x.dtype)
 
 
 def Make_Template_size_predictions(centers):

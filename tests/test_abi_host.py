@@ -81,6 +81,21 @@ def test_invalid_arguments_return_codes():
     assert L.tmr_split_acc_size(1, 100, 17, 33) == 128 * 32 * 64
     assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, None, None) == -1
     assert L.tmr_absmax(None, 4, 0, None, None) == -1
+    # masked maxpool: an empty selection (torch.max rejects it) or bits past the 3x3 window
+    assert L.tmr_maxpool3x3(None, 1, 4, 4, 0, None, None) == -1
+    assert L.tmr_maxpool3x3(None, 1, 4, 4, 1 << 9, None, None) == -1
+    assert L.tmr_maxpool3x3(None, 0, 4, 4, 0x1ff, None, None) == 0  # empty input: nothing to launch
+
+
+def test_tm_utils_host_helpers():
+    import torch
+    assert tmr_amd.calc_area([1.0, 2.0, 4.0, 7.0]) == 15.0
+    x = np.array([[1.0, 3.0], [2.0, 5.0]], np.float32)
+    np.testing.assert_array_equal(tmr_amd.map_normalization(x), (x - 1.0) / (4.0 + 1e-14))
+    t = tmr_amd.map_normalization(torch.from_numpy(x))
+    assert torch.equal(t, (torch.from_numpy(x) - 1.0) / (4.0 + 1e-14))
+    with pytest.raises(tmr_amd.TMRError):  # GPU only, no CPU fallback
+        tmr_amd.custom_shape_3x3_maxpool2d(torch.zeros(1, 1, 4, 4), [[1] * 3] * 3)
 
 
 def test_gpu_only_guard():

@@ -356,6 +356,42 @@ def _split(g, key):
     return out
 
 
+KERNELS = [[[1, 1, 1], [1, 1, 1], [1, 1, 1]], [[0, 0, 0], [0, 1, 0], [0, 0, 0]],
+           [[0, 1, 0], [0, 1, 0], [0, 1, 0]], [[0, 0, 0], [1, 1, 1], [0, 0, 0]],
+           [[0, 1, 0], [1, 1, 1], [0, 1, 0]], [[1, 0, 0], [0, 0, 0], [0, 0, 1]]]
+
+
+def _maxpool_reference(x, kernel):
+    """TM_utils.py:337-361 as written (F.unfold + mask + max), torch CPU."""
+    import torch.nn.functional as F
+    flat = torch.tensor(kernel, dtype=torch.bool).flatten()
+    N, C, H, W = x.shape
+    patches = F.unfold(x, kernel_size=3, padding=1).view(N, -1, 9, H, W)
+    return patches[:, :, flat, :, :].max(dim=2)[0]
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 7, 9), (1, 1, 1, 1), (1, 2, 128, 128), (3, 1, 2, 5)])
+def test_custom_shape_maxpool_vs_reference(shape):
+    """Bit-exact against the reference formulation for every adaptive
+    kernel shape (plus an off-centre one): negatives (the zero padding
+    wins at the border), exact ties, +-0 and a NaN."""
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.round(torch.randn(shape, generator=g) * 4) / 4  # many exact ties
+    x.view(-1)[::7] = -x.view(-1)[::7].abs() - 1
+    if x.numel() > 20:
+        x.view(-1)[5] = -0.0
+        x.view(-1)[11] = float("nan")
+    for k in KERNELS:
+        ref = _maxpool_reference(x, k)
+        got = tmr_amd.custom_shape_3x3_maxpool2d(x.to(DEV), k).cpu()
+        assert got.shape == ref.shape
+        assert torch.equal(torch.isnan(got), torch.isnan(ref)), k
+        m = ~torch.isnan(ref)
+        assert torch.equal(got[m], ref[m]), k
+    with pytest.raises(tmr_amd.TMRError):
+        tmr_amd.custom_shape_3x3_maxpool2d(x.to(DEV), [[0] * 3] * 3)
+
+
 def test_get_pred_boxes_golden(golden):
     """Bit-exact given identical score maps: feed the reference's own
     sigmoid output (input_is_prob) and compare every candidate."""
