@@ -1,4 +1,4 @@
-# r02i: VALU correlation kernel variants (old = previous build, new = this tree), parity
+# r02i/r02s: VALU correlation kernel variants (old = previous build, new = this tree), parity
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -269,6 +269,12 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
 constexpr int PADL = 20;  // >= 15 + 3 (max half-width + OFF), multiple of 4
 constexpr int PADR = 24;  // covers the window over-read past column W
 constexpr int TRY = 4;  // max tile rows (the LDS slack rows cover it)
+// rows kernel FMA form per template width: scalar v_fma_f32 up to this width
+// (no odd pairs to build; measured k = 3 1.79 vs 2.02 ms, k = 5 2.58 vs 2.65),
+// v_pk_fma_f32 on column pairs above it (k = 15 7.97 vs 10.81 ms; profiles/r02s_*)
+#ifndef TMR_XCORR_SCALAR_MAXW
+#define TMR_XCORR_SCALAR_MAXW 5
+#endif
 
 // (a.y, b.x) as ONE v_pk_mov_b32 (left to itself the compiler often builds
 // the odd pair with two v_mov_b32)
@@ -287,7 +293,7 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
     constexpr int NO = (OFF + KW + TRX - 2) / 2;   // odd pairs (x[2m+1], x[2m+2])
     for (int ii = 0; ii < TRY + h - 1; ++ii) {
         const f32x4 *xr = reinterpret_cast<const f32x4 *>(xs + (lrow0 + ii) * WS + lcol0);
-        f32x2 xe[2 * NV], xo[NO];
+        f32x2 xe[2 * NV];
         f32x4 v4[NV];
 #pragma unroll
         for (int j = 0; j < NV; ++j) v4[j] = xr[j];
@@ -303,6 +309,29 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
             xe[2 * j] = f32x2{v4[j].x, v4[j].y};
             xe[2 * j + 1] = f32x2{v4[j].z, v4[j].w};
         }
+        if constexpr (KW <= TMR_XCORR_SCALAR_MAXW) {
+        // scalar v_fma_f32 on the even-pair registers' halves: no odd pairs
+#pragma unroll
+        for (int r = 0; r < TRY; ++r) {
+            const int i = ii - r;
+            if (i < 0 || i >= h) continue;  // wave-uniform
+            const float *tr = tc + i * KW;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const float t = tr[j];
+#pragma unroll
+                for (int q = 0; q < TRX; ++q) {
+                    const int s0 = q + j + OFF;
+                    const float xv = (s0 & 1) ? xe[s0 >> 1].y : xe[s0 >> 1].x;
+                    if (q & 1)
+                        pa[r][q >> 1].y = fmaf(xv, t, pa[r][q >> 1].y);
+                    else
+                        pa[r][q >> 1].x = fmaf(xv, t, pa[r][q >> 1].x);
+                }
+            }
+        }
+        } else {
+        f32x2 xo[NO];
 #pragma unroll
         for (int m = 0; m < NO; ++m) xo[m] = odd_pair(xe[m], xe[m + 1]);
 #pragma unroll
@@ -321,6 +350,7 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
                     pa[r][q] = __builtin_elementwise_fma(xv2, tt, pa[r][q]);
                 }
             }
+        }
         }
     }
 }
