@@ -420,3 +420,23 @@ def test_stream_cli_tar_producer(tmp_path, capsys):
         assert va[4] == vb[4]
         np.testing.assert_allclose(va, vb, rtol=1e-12)
     assert out_a.splitlines()[0].startswith("CATEGORY") and out_a == out_b
+
+
+def test_sam_preprocessing():
+    """extract_feature.py:49-66: longest side to the target (int(x * s + 0.5)),
+    PIL bilinear, fp32 (x - mean) / std, zero pad right/bottom."""
+    from PIL import Image
+    rng = np.random.default_rng(3)
+    arr = rng.integers(0, 256, (30, 50, 3), dtype=np.uint8)
+    data = _png_bytes(arr, "RGB")
+    x = mr.preprocess_image_sam(data, 64)
+    assert x.shape == (1, 3, 64, 64) and x.dtype == np.float32
+    newh, neww = int(30 * (64 / 50) + 0.5), int(50 * (64 / 50) + 0.5)
+    assert (newh, neww) == (38, 64)
+    r = np.asarray(Image.fromarray(arr).resize((neww, newh), Image.Resampling.BILINEAR)).astype(np.float32)
+    mean = np.float32([123.675, 116.28, 103.53])
+    std = np.float32([58.395, 57.12, 57.375])
+    ref = (r - mean) / std
+    np.testing.assert_array_equal(x[0, :, :newh, :neww], ref.transpose(2, 0, 1))
+    assert not x[0, :, newh:, :].any()
+    assert mr.preprocess_image_sam(b"garbage") is None
