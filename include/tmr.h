@@ -135,13 +135,15 @@ int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *temp
 /* Operand prep of the MFMA correlation: per (unit u, channel c) template
  * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
  * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <
- * 2^14), written as zero-padded rows (TMR_TSPLIT_ROW fp16 each, tap j at
- * column TMR_TSPLIT_PAD + j): row i of term k (0 hi, 1 lo) of (u, c) is row
- * (C * row_offset(u) + c * ht) * 2 + k * ht + i; then e int32[U][C].
- * total_rows = sum of ht over the units; size in bytes from
- * tmr_template_split_size. */
-#define TMR_TSPLIT_ROW 96
-#define TMR_TSPLIT_PAD 24
+ * 2^14), written as the kernel's MFMA A fragments: with nk(wt) = 1 if
+ * 16 + s + wt - 1 <= 32 else 2 (pw = wt/2, s = 8*ceil(pw/8) - pw) K blocks
+ * per template row, the 1-KB fragment (64 lanes x 8 fp16; lane m + 16 g holds
+ * T[i][8g + 32b + q - m - s], q = 0..7, zero outside [0, wt)) of row i, block
+ * b, term k (0 hi, 1 lo) of (u, c) is fragment number
+ * (C * row_offset(u) + c * ht * nk) * 2 + (i * nk + b) * 2 + k; then e
+ * int32[U][C].  row_offset(u) = sum over earlier units of ht * nk(wt) and
+ * total_rows = that sum over all units (tmr_unit_t.row_offset, set by the
+ * host); size in bytes from tmr_template_split_size. */
 int64_t tmr_template_split_size(int U, int C, int64_t total_rows);
 int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
                        int64_t total_rows, void *out, void *stream);

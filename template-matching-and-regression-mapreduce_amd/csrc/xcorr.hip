@@ -545,18 +545,25 @@ __device__ __forceinline__ float block_max(float v, float *red) {
 
 // Per (unit, channel) split of the exemplar templates for the MFMA kernel
 // (tmr_template_split): t * 2^-et = th + tl (fp16) with 2^-et the power-of-two
-// scale of the template's own max |t| (max |t| 2^-et < 2^14), written as
-// zero-padded rows so that the kernel's A fragment -- 8 consecutive taps
-// T[i][8g + 32nk - m - s ..] for lane (m, g) -- is ONE 16-B load per lane
-// with no bounds checks.  One wave per (unit, channel).
-constexpr int TROW = TMR_TSPLIT_ROW;
-constexpr int TOFF = TMR_TSPLIT_PAD;
-static_assert(TOFF >= 15 + 7 && TOFF + 64 + 8 <= TROW, "padded template rows");
+// scale of the template's own max |t| (max |t| 2^-et < 2^14), written as the
+// kernel's A fragments themselves: for template row i, K block nk and term
+// (hi, lo), 64 lanes x 16 B in lane order, lane (m, g) holding the taps
+// T[i][8g + 32nk + q - m - s], q = 0..7 (zero outside [0, w)).  The kernel's
+// A load is then one aligned, contiguous 1-KB wave read.  (Loading the same
+// 16-B windows at 2-B-aligned offsets out of padded template rows -- round 2's
+// first layout -- cost 17-21% of the kernel at k = 15: profiles/r02u_*.)
+// One wave per (unit, channel).
+constexpr int AFRAG = 64 * 16;  // bytes per (row, nk, term) fragment
+
+__host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per template row
+    const int pw = w / 2, s = ((pw + 7) & ~7) - pw;
+    return 16 + s + w - 1 <= 32 ? 1 : 2;
+}
 
 __global__ __launch_bounds__(256) void template_split_kernel(const float *__restrict__ tmpl,
                                                              const tmr_unit_t *__restrict__ units, int U,
                                                              int C, int64_t total_rows,
-                                                             _Float16 *__restrict__ rows,
+                                                             char *__restrict__ frags,
                                                              int32_t *__restrict__ exps) {
     const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
@@ -570,36 +577,49 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     int et;
     const float st = pow2_scale(m, et);
-    _Float16 *dst = rows + ((int64_t)C * un.row_offset + (int64_t)c * h) * 2 * TROW;
-    for (int e = lane; e < 2 * h * TROW; e += 64) {
-        const int term = e >= h * TROW, r = e - term * h * TROW, i = r / TROW, j = r % TROW - TOFF;
-        const float x = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
-        const _Float16 hx = (_Float16)x;
-        dst[e] = term ? (_Float16)(x - (float)hx) : hx;
-    }
+    const int nk_u = tsplit_nk(w), pw = w / 2, s = ((pw + 7) & ~7) - pw;
+    const int mm = lane & 15, g = lane >> 4;
+    char *dst = frags + ((int64_t)C * un.row_offset + (int64_t)c * h * nk_u) * 2 * AFRAG + lane * 16;
+    for (int i = 0; i < h; ++i)
+        for (int nk = 0; nk < nk_u; ++nk) {
+            h8 hi, lo;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int j = 8 * g + 32 * nk + q - mm - s;
+                const float x = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
+                const _Float16 hx = (_Float16)x;
+                hi[q] = hx;
+                lo[q] = (_Float16)(x - (float)hx);
+            }
+            char *f = dst + (size_t)((i * nk_u + nk) * 2) * AFRAG;
+            *reinterpret_cast<h8 *>(f) = hi;
+            *reinterpret_cast<h8 *>(f + AFRAG) = lo;
+        }
     if (lane == 0) exps[(int64_t)u * C + c] = et;
 }
 
 // one unit over the band: acc[t] += sum_i A_i B_i over the wave's NTW tiles
 // (tile cols tcol0 + WPR t).  The A fragments -- lane (m, g): taps
-// T[i][8g + 32nk + q - m - s], q = 0..7 -- are single 16-B (2-B aligned)
-// global loads from the zero-padded split rows (L2 resident), issued PF
-// template rows ahead of their MFMAs.  (Measured: staging them through an
-// LDS table per row chunk, with its two barriers per chunk, was slower at
-// every k >= 11; profiles/r02b_kbench_xcorr_*.)
+// T[i][8g + 32nk + q - m - s], q = 0..7 -- are aligned 16-B lane loads of the
+// pre-expanded fragments (tmr_template_split; arow = this lane's slot of
+// row 0), issued PF template rows ahead of their MFMAs.  (Measured: staging
+// them through an LDS table per row chunk, with its two barriers per chunk,
+// was slower at every k >= 11; profiles/r02b_kbench_xcorr_*.)
 template <int NTW, int NK, int WPR>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
-    constexpr int PF = 1;  // prefetch distance (template rows; 2 costs a wave per SIMD in VGPRs)
+    constexpr int PF = 1;  // prefetch distance (template rows; 2 and 3 measured equal, r02t)
     h8 ah[PF][NK], al[PF][NK];
-    const size_t tstride = (size_t)h * TROW * 2;  // bytes from the hi rows to the lo rows
+    auto afrag = [&](int i, int nk, int term) -> h8 {
+        return *reinterpret_cast<const h8 *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
+    };
 #pragma unroll
     for (int p = 0; p < PF; ++p)
         if (p < h) {
 #pragma unroll
             for (int nk = 0; nk < NK; ++nk) {
-                ah[p][nk] = *reinterpret_cast<const h8 *>(arow + (size_t)p * TROW * 2 + 64 * nk);
-                al[p][nk] = *reinterpret_cast<const h8 *>(arow + tstride + (size_t)p * TROW * 2 + 64 * nk);
+                ah[p][nk] = afrag(p, nk, 0);
+                al[p][nk] = afrag(p, nk, 1);
             }
         }
     for (int i0 = 0; i0 < h; i0 += PF) {
@@ -617,8 +637,8 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
             if (i + PF < h) {
 #pragma unroll
                 for (int nk = 0; nk < NK; ++nk) {
-                    ah[p][nk] = *reinterpret_cast<const h8 *>(arow + (size_t)(i + PF) * TROW * 2 + 64 * nk);
-                    al[p][nk] = *reinterpret_cast<const h8 *>(arow + tstride + (size_t)(i + PF) * TROW * 2 + 64 * nk);
+                    ah[p][nk] = afrag(i + PF, nk, 0);
+                    al[p][nk] = afrag(i + PF, nk, 1);
                 }
             }
 #pragma unroll
@@ -721,8 +741,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
 #pragma unroll
         for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         if (row_live) {
-            const char *arow = reinterpret_cast<const char *>(
-                trows + ((int64_t)a.C * roff + (int64_t)c * h) * 2 * TROW + TOFF + 8 * g - l16 - s);
+            const char *arow = reinterpret_cast<const char *>(trows) +
+                               ((int64_t)a.C * roff + (int64_t)c * h * tsplit_nk(w)) * 2 * AFRAG + lane * 16;
             const int rb = tr * 16 + l16 + hg - ph;  // LDS row of output row (yb0 + 16 tr + l16) at i = 0
             if (16 + s + w - 1 <= 32)
                 mfma_unit<NTW, 1, WPR>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
@@ -859,7 +879,8 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
     const size_t lds = 2 * (size_t)m.LR * m.SB + 64;
     const unsigned nblk = (unsigned)((nlog + 7) / 8 * 8);
     const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
-    const int32_t *texp = reinterpret_cast<const int32_t *>(trows + (int64_t)a.C * total_rows * 2 * TROW);
+    const int32_t *texp = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
+                                                            (int64_t)a.C * total_rows * 2 * AFRAG);
     (void)U;
     const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
     return launch_mfma_w<2>(a, m, lds, nblk, s, trows, texp, nv4);
@@ -867,17 +888,17 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
 
 extern "C" int64_t tmr_template_split_size(int U, int C, int64_t total_rows) {
     if (U <= 0 || C <= 0 || total_rows <= 0) return -1;
-    return (int64_t)C * total_rows * 2 * TROW * 2 + 4 * (int64_t)U * C;
+    return (int64_t)C * total_rows * 2 * AFRAG + 4 * (int64_t)U * C;
 }
 
 extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
                                   int64_t total_rows, void *out, void *stream) {
     TMR_REQUIRE(templates && units && out && U > 0 && C > 0 && total_rows > 0);
-    _Float16 *rows = reinterpret_cast<_Float16 *>(out);
-    int32_t *ex = reinterpret_cast<int32_t *>(rows + (int64_t)C * total_rows * 2 * TROW);
+    char *frags = reinterpret_cast<char *>(out);
+    int32_t *ex = reinterpret_cast<int32_t *>(frags + (int64_t)C * total_rows * 2 * AFRAG);
     const int64_t waves = (int64_t)U * C;
     hipLaunchKernelGGL(template_split_kernel, dim3((unsigned)tmr_cdiv(waves, 4)), dim3(256), 0,
-                       tmr_stream(stream), templates, units, U, C, total_rows, rows, ex);
+                       tmr_stream(stream), templates, units, U, C, total_rows, frags, ex);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

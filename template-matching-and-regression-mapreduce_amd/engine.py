@@ -62,7 +62,7 @@ class PathConfig:
 
 # Correlation-kernel crossover (tmr_xcorr_algo), from the measured launch
 # times of both kernels per template side k (HIP events, kbench_xcorr,
-# profiles/r02c_kbench_xcorr_sweep{128,192}.jsonl), as ms per unit at the
+# profiles/r02w_sweep{128,192}.jsonl), as ms per unit at the
 # 512 x 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
 # exemplars at 128^2; the image's band staging is shared by 3 units) and
 # E = 16 (8 images x 16 exemplars at 192^2, times / 2.25 for the area).
@@ -71,16 +71,14 @@ class PathConfig:
 # VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
 # crossover); at E = 16 MFMA wins from k = 9 on.
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
-_T128 = {  # ms per 192 units (E = 3), r02c sweep
-    "valu": (1.603, 1.973, 2.488, 3.546, 4.066, 5.758, 6.657, 9.247, 10.356, 14.634, 14.984, 20.271,
-             20.318, 28.515, 27.311, 37.380),
-    "mfma": (2.252, 2.970, 3.653, 4.306, 5.000, 5.683, 6.366, 7.099, 7.832, 14.587, 16.013, 17.468,
-             18.923, 20.383, 21.830, 23.335),
+_T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
+    "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
+    "mfma": (1.962, 2.577, 3.189, 3.755, 4.350, 4.796, 5.407, 5.987, 6.666, 10.969, 12.070, 13.200, 14.328, 15.542, 16.785, 17.876),
 }
 _K192 = (3, 9, 15, 21, 31)
-_T192 = {  # ms per 128 units (E = 16) at 192^2, r02c sweep
-    "valu": (2.697, 6.027, 14.634, 22.891, 62.326),
-    "mfma": (3.442, 5.849, 8.235, 16.312, 23.813),
+_T192 = {  # ms per 128 units (E = 16) at 192^2, r02w sweep
+    "valu": (2.539, 6.081, 13.025, 22.462, 51.697),
+    "mfma": (3.192, 5.520, 7.462, 15.101, 22.257),
 }
 XCORR_COST = {
     a: (np.asarray(_T128[a]) / 192.0,
@@ -91,9 +89,10 @@ XCORR_COST = {
 # rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
 # units when an image has few of them: measured 1.13x the per-k sum at the
 # config-B 3..15 mix with 3 units per image (5.57 ms vs 4.91,
-# profiles/r02b_kbench_xcorr_mixB*), 1.46x for the k >= 11 units of that batch
-# (~2 per image; profiles/r02c_bench_B* by_class); the VALU kernel's mixes match
-# its per-k sums (4.75 vs 4.72).  Empirical: 1 + 0.4 / units-per-image.
+# profiles/r02b_kbench_xcorr_mixB*; 1.10x after the aligned-fragment change,
+# 4.75 vs 4.30, profiles/r02w_mixB.jsonl), 1.46x for the k >= 11 units of that
+# batch (~2 per image; profiles/r02c_bench_B* by_class); the VALU kernel's
+# mixes run 1.00-1.04x its per-k sums.  Empirical: 1 + 0.4 / units-per-image.
 XCORR_MFMA_MIX = 0.4
 
 
@@ -555,7 +554,7 @@ class TMREngine:
         tsplit = None
         if algo != XCORR_ALGOS["valu"] and tfl > 0:
             # hi/lo fp16 operands of the MFMA correlation (per (unit, channel) scale)
-            rows = int(units["ht"].sum())
+            rows = host.tsplit_rows(units)
             tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
             call("tmr_template_split", ptr(tmpl), ptr(units_d), U, C, rows, ptr(tsplit), stream())
         call("tmr_xcorr_algo", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,

@@ -65,6 +65,20 @@ def prototype_box(box, H: int, W: int) -> np.ndarray:
     return b
 
 
+def tsplit_nk(wt: int) -> int:
+    """K blocks of 32 per template row in the MFMA correlation's A fragments
+    (include/tmr.h, tmr_template_split): 1 when the 16-column Toeplitz band of
+    a w-wide template row (shifted by s to a 16-B aligned window) fits 32."""
+    pw = int(wt) // 2
+    s = ((pw + 7) & ~7) - pw
+    return 1 if 16 + s + int(wt) - 1 <= 32 else 2
+
+
+def tsplit_rows(units: np.ndarray) -> int:
+    """total_rows of tmr_template_split: sum of ht * tsplit_nk(wt)."""
+    return int(sum(int(h) * tsplit_nk(int(w)) for h, w in zip(units["ht"], units["wt"])))
+
+
 def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int,
                 template_type: str = "roi_align"):
     """tmr_unit_t array for U units.  Returns (units, template_floats, max_ht, max_wt)."""
@@ -88,7 +102,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         units["tmpl_offset"][u] = off
         units["row_offset"][u] = rows
         off += C * ht * wt
-        rows += ht
+        rows += ht * tsplit_nk(wt)
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
     return units, off, max_ht, max_wt
 

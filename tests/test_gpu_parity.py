@@ -621,7 +621,7 @@ def test_xcorr_mfma_vs_oracle(H, W, C, kmax):
     U = len(ui)
     scale = torch.tensor([0.75], device=DEV)
     lib = tmr_amd._lib.load()
-    rows = int(units["ht"].sum())
+    rows = host.tsplit_rows(units)
     tsplit = torch.empty(lib.tmr_template_split_size(U, C, rows), device=DEV, dtype=torch.uint8)
     call("tmr_template_split", ptr(tmpl), ptr(ud), U, C, rows, ptr(tsplit), stream())
     outs = {}
