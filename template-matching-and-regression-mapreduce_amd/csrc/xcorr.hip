@@ -565,15 +565,29 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                                                              int C, int64_t total_rows,
                                                              char *__restrict__ frags,
                                                              int32_t *__restrict__ exps) {
+    // the wave's template through LDS (coalesced global reads once; the
+    // fragments' lane-shifted taps are then LDS reads, not 8 scattered global
+    // loads per lane and fragment)
+    __shared__ float tsh[4][31 * 31];
     const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wid >= (int64_t)U * C) return;  // wave-uniform
     const int u = (int)(wid / C), c = (int)(wid % C);
     const tmr_unit_t un = units[u];
     const int h = un.ht, w = un.wt, hw = h * w;
-    const float *t = tmpl + un.tmpl_offset + (int64_t)c * hw;
+    const float *tg = tmpl + un.tmpl_offset + (int64_t)c * hw;
+    const bool staged = hw <= 31 * 31;  // larger templates (not MFMA shapes) read global memory
+    float *ts = tsh[threadIdx.x >> 6];
     float m = 0.0f;
-    for (int e = lane; e < hw; e += 64) m = fmaxf(m, fabsf(t[e]));
+    for (int e = lane; e < hw; e += 64) {
+        const float v = tg[e];
+        if (staged) ts[e] = v;
+        m = fmaxf(m, fabsf(v));
+    }
+    const float *t = staged ? ts : tg;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     int et;
     const float st = pow2_scale(m, et);
