@@ -1,4 +1,4 @@
-# r02v: MFMA correlation with pre-expanded aligned A fragments (this tree) vs
+# r02v/r02z: MFMA correlation variants (old = previous build, new = this tree): parity, per-k and mixed timings
 # the padded-row layout (libtmr_old.so): parity, per-k and mixed timings
 set -o pipefail
 mkdir -p gpurun_out
