@@ -328,9 +328,12 @@ def main():
         xs = float(np.mean(xc_ms)) / 1e3
         xk = eng.last_xcorr_algo
         out["roofline_xcorr"] = {
-            "kernel": ("tmr_xcorr_algo MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
-                       "v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if xk == "mfma" else
-                       "tmr_xcorr_algo VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
+            "kernel": ("tmr_xcorr_prec MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
+                       + ("v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if prec == "fp32" else
+                          "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
+                                                                     else ("f16", "scaled fp16")))
+                       if xk == "mfma" else
+                       "tmr_xcorr_prec VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
                       + " + /hw + pad + scale + max|f_TM|; kernel chosen by the measured per-k cost model "
                         "(engine.XCORR_COST)",
             "algo": xk,

@@ -132,6 +132,19 @@ int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *temp
                    const float *scale, int squeeze, float *out, float *relu_out, float *work,
                    float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
                    int min_k, void *stream);
+/* Same with the MFMA kernel's operand precision chosen (prec, the TMR_PREC_*
+ * codes below): TMR_PREC_F16X3 is tmr_xcorr_algo (the fp32 path's 1e-5
+ * contract); TMR_PREC_BF16 / TMR_PREC_F16 run the MFMA kernel on ONE bf16 /
+ * scaled-fp16 term per product with fp32 accumulation -- the bf16 MFMA path of
+ * BASELINE config C (north_star "within a stated bf16 tolerance": <= 1e-2
+ * normwise, tests/test_gpu_parity.py).  The VALU kernels are fp32 whatever
+ * prec says.  tmpl_split must come from tmr_template_split_prec with the same
+ * prec (TMR_PREC_F16 and TMR_PREC_F16X3 fragments are identical). */
+int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
+                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
+                   const float *scale, int squeeze, float *out, float *relu_out, float *work,
+                   float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
+                   int min_k, int prec, void *stream);
 /* Operand prep of the MFMA correlation: per (unit u, channel c) template
  * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
  * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <
@@ -147,6 +160,11 @@ int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *temp
 int64_t tmr_template_split_size(int U, int C, int64_t total_rows);
 int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
                        int64_t total_rows, void *out, void *stream);
+/* The same fragments in the operand format of tmr_xcorr_prec's prec:
+ * TMR_PREC_BF16 writes bf16 hi (and the bf16 residual in the lo slot);
+ * TMR_PREC_F16X3 / TMR_PREC_F16 are tmr_template_split. */
+int tmr_template_split_prec(const float *templates, const tmr_unit_t *units, int U, int C,
+                            int64_t total_rows, int prec, void *out, void *stream);
 
 /* ---- (a10+a11+a12) conv stack ---------------------------------------------
  * Implicit-GEMM kxk conv over the virtual channel concat

@@ -7,7 +7,7 @@ per unit, f_TM written), FLOPs = 2*C*(H-k+1)^2*k^2 per unit; HBM peak 8 TB/s,
 fp32 VALU peak 157.3 TF.  --mixed runs the config-B mix (k uniform 3..15).
 
     python profiles/kbench_xcorr.py [--images 64] [--E 3] [--H 128] [--algos valu,mfma]
-                                    [--ks 1,3,5,...] [--mixed]
+                                    [--ks 1,3,5,...] [--mixed] [--precision fp32|bf16|f16]
 """
 import argparse
 import json
@@ -47,11 +47,12 @@ def main():
     ap.add_argument("--mixed", action="store_true", help="config-B mix: k uniform over 3..15")
     ap.add_argument("--kmin", type=int, default=3)
     ap.add_argument("--kmax", type=int, default=15)
+    ap.add_argument("--precision", default="fp32", help="MFMA operand precision: fp32 (3-term), bf16, f16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, H = a.images, 512, a.H
     P = {k: v.to(dev) for k, v in synth.reference_state_dict(0).items()}
-    eng = tmr.TMREngine(P, tmr.PathConfig())
+    eng = tmr.TMREngine(P, tmr.PathConfig(precision=a.precision))
     g = torch.Generator(device=dev).manual_seed(0)
     fp = torch.randn((B, C, H, H), device=dev, generator=g)
     ui = np.repeat(np.arange(B), a.E)
@@ -73,7 +74,7 @@ def main():
             except tmr.TMRError as e:
                 print(json.dumps({"algo": algo, "k": name, "error": str(e)}), flush=True)
                 continue
-            print(json.dumps({"algo": algo, "k": name, "images": B, "E": a.E, "H": H, "ms": round(ms, 4),
+            print(json.dumps({"algo": algo, "prec": a.precision, "k": name, "images": B, "E": a.E, "H": H, "ms": round(ms, 4),
                               "hbm_gbps": round(nbytes / ms / 1e6, 1),
                               "hbm_frac": round(nbytes / ms / 1e6 / 8000.0, 4),
                               "tflops": round(flops / ms / 1e9, 2),

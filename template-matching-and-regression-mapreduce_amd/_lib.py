@@ -63,8 +63,11 @@ SIGNATURES = {
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
     "tmr_xcorr_algo": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
                             _I, _I, _P]),
+    "tmr_xcorr_prec": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
+                            _I, _I, _I, _P]),
     "tmr_template_split_size": (_L, [_I, _I, _L]),
     "tmr_template_split": (_I, [_P, _P, _I, _I, _L, _P, _P]),  # (..., total_rows, out, stream)
+    "tmr_template_split_prec": (_I, [_P, _P, _I, _I, _L, _I, _P, _P]),  # (..., total_rows, prec, out, stream)
     "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
     "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),

@@ -516,6 +516,32 @@ constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+
+// Operand precision of the MFMA kernel (PM, the TMR_PREC_* codes):
+// TMR_PREC_F16X3 the fp32-grade 3-term fp16 split (1e-5 contract);
+// TMR_PREC_BF16 / TMR_PREC_F16 ONE 16-bit term, fp32 accumulation (the bf16
+// path of config C, 1e-2 contract): the lo plane, the lo fragments and two
+// of the three MFMAs drop out.
+template <int PM> struct XOp {
+    typedef _Float16 E;
+    typedef h8 V8;
+    typedef h4 V4;
+    static constexpr bool SPLIT = PM == TMR_PREC_F16X3;
+};
+template <> struct XOp<TMR_PREC_BF16> {
+    typedef __bf16 E;
+    typedef b8 V8;
+    typedef b4 V4;
+    static constexpr bool SPLIT = false;
+};
+__device__ __forceinline__ f32x4 xmma(h8 a, h8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 xmma(b8 a, b8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 struct MArgs {
     int SB;     // LDS plane row stride in bytes (32 mod 64)
@@ -562,7 +588,7 @@ __host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per templat
 
 __global__ __launch_bounds__(256) void template_split_kernel(const float *__restrict__ tmpl,
                                                              const tmr_unit_t *__restrict__ units, int U,
-                                                             int C, int64_t total_rows,
+                                                             int C, int64_t total_rows, int bf,
                                                              char *__restrict__ frags,
                                                              int32_t *__restrict__ exps) {
     // the wave's template through LDS (coalesced global reads once; the
@@ -596,18 +622,32 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
     char *dst = frags + ((int64_t)C * un.row_offset + (int64_t)c * h * nk_u) * 2 * AFRAG + lane * 16;
     for (int i = 0; i < h; ++i)
         for (int nk = 0; nk < nk_u; ++nk) {
-            h8 hi, lo;
+            float x[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int j = 8 * g + 32 * nk + q - mm - s;
-                const float x = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
-                const _Float16 hx = (_Float16)x;
-                hi[q] = hx;
-                lo[q] = (_Float16)(x - (float)hx);
+                x[q] = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
             }
             char *f = dst + (size_t)((i * nk_u + nk) * 2) * AFRAG;
-            *reinterpret_cast<h8 *>(f) = hi;
-            *reinterpret_cast<h8 *>(f + AFRAG) = lo;
+            if (bf) {  // wave-uniform: bf16 hi / residual (the one-term bf16 MFMA reads hi only)
+                b8 hi, lo;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    hi[q] = (__bf16)x[q];
+                    lo[q] = (__bf16)(x[q] - (float)hi[q]);
+                }
+                *reinterpret_cast<b8 *>(f) = hi;
+                *reinterpret_cast<b8 *>(f + AFRAG) = lo;
+            } else {
+                h8 hi, lo;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    hi[q] = (_Float16)x[q];
+                    lo[q] = (_Float16)(x[q] - (float)hi[q]);
+                }
+                *reinterpret_cast<h8 *>(f) = hi;
+                *reinterpret_cast<h8 *>(f + AFRAG) = lo;
+            }
         }
     if (lane == 0) exps[(int64_t)u * C + c] = et;
 }
@@ -619,13 +659,15 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
 // row 0), issued PF template rows ahead of their MFMAs.  (Measured: staging
 // them through an LDS table per row chunk, with its two barriers per chunk,
 // was slower at every k >= 11; profiles/r02b_kbench_xcorr_*.)
-template <int NTW, int NK, int WPR>
+template <int NTW, int NK, int WPR, int PM>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
+    typedef typename XOp<PM>::V8 V;
+    constexpr bool SPLIT = XOp<PM>::SPLIT;
     constexpr int PF = 1;  // prefetch distance (template rows; 2 and 3 measured equal, r02t)
-    h8 ah[PF][NK], al[PF][NK];
-    auto afrag = [&](int i, int nk, int term) -> h8 {
-        return *reinterpret_cast<const h8 *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
+    V ah[PF][NK], al[PF][NK];
+    auto afrag = [&](int i, int nk, int term) -> V {
+        return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
     };
 #pragma unroll
     for (int p = 0; p < PF; ++p)
@@ -633,7 +675,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
 #pragma unroll
             for (int nk = 0; nk < NK; ++nk) {
                 ah[p][nk] = afrag(p, nk, 0);
-                al[p][nk] = afrag(p, nk, 1);
+                if (SPLIT) al[p][nk] = afrag(p, nk, 1);
             }
         }
     for (int i0 = 0; i0 < h; i0 += PF) {
@@ -642,17 +684,17 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
             const int i = i0 + p;
             if (i >= h) break;
             const char *rh = Fh + (size_t)(rb + i) * SB, *rl = Fl + (size_t)(rb + i) * SB;
-            h8 ch[NK], cl[NK];
+            V ch[NK], cl[NK];
 #pragma unroll
             for (int nk = 0; nk < NK; ++nk) {
                 ch[nk] = ah[p][nk];
-                cl[nk] = al[p][nk];
+                if (SPLIT) cl[nk] = al[p][nk];
             }
             if (i + PF < h) {
 #pragma unroll
                 for (int nk = 0; nk < NK; ++nk) {
                     ah[p][nk] = afrag(i + PF, nk, 0);
-                    al[p][nk] = afrag(i + PF, nk, 1);
+                    if (SPLIT) al[p][nk] = afrag(i + PF, nk, 1);
                 }
             }
 #pragma unroll
@@ -660,22 +702,28 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
 #pragma unroll
                 for (int t = 0; t < NTW; ++t) {
                     const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-                    const h8 bh = *reinterpret_cast<const h8 *>(rh + colb);
-                    const h8 bl = *reinterpret_cast<const h8 *>(rl + colb);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[nk], bh, acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[nk], bl, acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl[nk], bh, acc[t], 0, 0, 0);
+                    const V bh = *reinterpret_cast<const V *>(rh + colb);
+                    acc[t] = xmma(ch[nk], bh, acc[t]);
+                    if (SPLIT) {
+                        const V bl = *reinterpret_cast<const V *>(rl + colb);
+                        acc[t] = xmma(ch[nk], bl, acc[t]);
+                        acc[t] = xmma(cl[nk], bh, acc[t]);
+                    }
                 }
             }
         }
     }
 }
 
-template <int NTW, int NV4, int TRB>
+template <int NTW, int NV4, int TRB, int PM>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
                                                        const tmr_unit_t *__restrict__ units) {
+    typedef typename XOp<PM>::E E;
+    typedef typename XOp<PM>::V4 V4;
+    constexpr bool SPLIT = XOp<PM>::SPLIT;
+    constexpr int NPL = SPLIT ? 2 : 1;  // staged planes (hi, lo)
     constexpr int WPR = 4 / TRB;  // waves per tile row
     constexpr int BR = 16 * TRB;  // output rows per block
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -689,8 +737,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     const int u_beg = __builtin_amdgcn_readfirstlane(a.img_units[img]);
     const int u_end = __builtin_amdgcn_readfirstlane(a.img_units[img + 1]);
     if (u_beg >= u_end) return;
-    char *Fh = smem, *Fl = smem + (size_t)LR * SB;
-    float *red = reinterpret_cast<float *>(smem + 2 * (size_t)LR * SB);
+    char *Fh = smem, *Fl = smem + (size_t)LR * SB;  // Fl: F16X3 only
+    float *red = reinterpret_cast<float *>(smem + NPL * (size_t)LR * SB);
     const int tid = threadIdx.x;
     const int yb0 = band * BR, yb1 = min(yb0 + BR, H);
     const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
@@ -714,8 +762,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     {
         const int pr = SB / 16 - W / 8;   // 16-B pieces of pad per row (2 left, rest right)
         const float rpr = 1.0f / (float)pr;
-        for (int e = tid; e < 2 * LR * pr; e += NT) {
-            const int pl = e & 1, rr = e >> 1;
+        for (int e = tid; e < NPL * LR * pr; e += NT) {
+            const int pl = SPLIT ? e & 1 : 0, rr = SPLIT ? e >> 1 : e;
             const int r = (int)(((float)rr + 0.5f) * rpr), j = rr - r * pr;
             const int col = j < MPADL / 8 ? 8 * j : W + 8 * j;
             *reinterpret_cast<h8 *>((pl ? Fl : Fh) + (size_t)r * SB + 2 * col) = h8{};
@@ -729,12 +777,14 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         if (e >= n4) break;
         const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
         const float x0 = v[k].x * sf, x1 = v[k].y * sf, x2 = v[k].z * sf, x3 = v[k].w * sf;
-        const h4 hv = {(_Float16)x0, (_Float16)x1, (_Float16)x2, (_Float16)x3};
-        const h4 lv = {(_Float16)(x0 - (float)hv[0]), (_Float16)(x1 - (float)hv[1]),
-                       (_Float16)(x2 - (float)hv[2]), (_Float16)(x3 - (float)hv[3])};
+        const V4 hv = {(E)x0, (E)x1, (E)x2, (E)x3};
         const size_t off = (size_t)lr * SB + 2 * (MPADL + 4 * cc);
-        *reinterpret_cast<h4 *>(Fh + off) = hv;
-        *reinterpret_cast<h4 *>(Fl + off) = lv;
+        *reinterpret_cast<V4 *>(Fh + off) = hv;
+        if (SPLIT) {
+            const V4 lv = {(E)(x0 - (float)hv[0]), (E)(x1 - (float)hv[1]), (E)(x2 - (float)hv[2]),
+                           (E)(x3 - (float)hv[3])};
+            *reinterpret_cast<V4 *>(Fl + off) = lv;
+        }
     }
     __syncthreads();
 
@@ -759,9 +809,9 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                                ((int64_t)a.C * roff + (int64_t)c * h * tsplit_nk(w)) * 2 * AFRAG + lane * 16;
             const int rb = tr * 16 + l16 + hg - ph;  // LDS row of output row (yb0 + 16 tr + l16) at i = 0
             if (16 + s + w - 1 <= 32)
-                mfma_unit<NTW, 1, WPR>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+                mfma_unit<NTW, 1, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
             else
-                mfma_unit<NTW, 2, WPR>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+                mfma_unit<NTW, 2, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
         }
         // ---- epilogue: exact unscale, correctly rounded /(h*w), scale, pad mask
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
@@ -847,28 +897,28 @@ static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
     return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
 }
 
-template <int NTW, int NV4, int TRB>
+template <int NTW, int NV4, int TRB, int PM>
 static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp) {
-    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB>;
+    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return TMR_E_HIP;
-    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB>), dim3(nblk), dim3(NT), lds, s, a, m, trows, texp,
-                       a.out, a.units);
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
+                       texp, a.out, a.units);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
 
-template <int TRB>
+template <int TRB, int PM>
 static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp, int nv4) {
     const int ntw = a.W / 16 / (4 / TRB);
     switch (ntw) {
-#define TMR_NTW(K)                                                                       \
-    case K:                                                                              \
-        return nv4 == 8 ? launch_mfma_t<K, 8, TRB>(a, m, lds, nblk, s, trows, texp)      \
-                        : launch_mfma_t<K, 16, TRB>(a, m, lds, nblk, s, trows, texp);
+#define TMR_NTW(K)                                                                         \
+    case K:                                                                                \
+        return nv4 == 8 ? launch_mfma_t<K, 8, TRB, PM>(a, m, lds, nblk, s, trows, texp)    \
+                        : launch_mfma_t<K, 16, TRB, PM>(a, m, lds, nblk, s, trows, texp);
         TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8)
 #undef TMR_NTW
         default: return TMR_E_UNSUPPORTED;
@@ -876,7 +926,7 @@ static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
 }
 
 static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, int max_wt,
-                       const void *tmpl_split, int64_t total_rows) {
+                       const void *tmpl_split, int64_t total_rows, int prec) {
     MArgs m;
     // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
     // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*)
@@ -890,14 +940,19 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
     const int64_t nlog = (int64_t)m.nband * a.C * B;
     TMR_REQUIRE(nlog < (1LL << 31) - 8);
     m.nlog = (int)nlog;
-    const size_t lds = 2 * (size_t)m.LR * m.SB + 64;
+    const size_t lds = (prec == TMR_PREC_F16X3 ? 2 : 1) * (size_t)m.LR * m.SB + 64;
     const unsigned nblk = (unsigned)((nlog + 7) / 8 * 8);
     const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
     const int32_t *texp = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
                                                             (int64_t)a.C * total_rows * 2 * AFRAG);
     (void)U;
     const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
-    return launch_mfma_w<2>(a, m, lds, nblk, s, trows, texp, nv4);
+    switch (prec) {
+        case TMR_PREC_F16X3: return launch_mfma_w<2, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_BF16: return launch_mfma_w<2, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_F16: return launch_mfma_w<2, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp, nv4);
+        default: return TMR_E_INVALID;
+    }
 }
 
 extern "C" int64_t tmr_template_split_size(int U, int C, int64_t total_rows) {
@@ -905,27 +960,35 @@ extern "C" int64_t tmr_template_split_size(int U, int C, int64_t total_rows) {
     return (int64_t)C * total_rows * 2 * AFRAG + 4 * (int64_t)U * C;
 }
 
-extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
-                                  int64_t total_rows, void *out, void *stream) {
+extern "C" int tmr_template_split_prec(const float *templates, const tmr_unit_t *units, int U, int C,
+                                       int64_t total_rows, int prec, void *out, void *stream) {
     TMR_REQUIRE(templates && units && out && U > 0 && C > 0 && total_rows > 0);
+    TMR_REQUIRE(prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16);
     char *frags = reinterpret_cast<char *>(out);
     int32_t *ex = reinterpret_cast<int32_t *>(frags + (int64_t)C * total_rows * 2 * AFRAG);
     const int64_t waves = (int64_t)U * C;
     hipLaunchKernelGGL(template_split_kernel, dim3((unsigned)tmr_cdiv(waves, 4)), dim3(256), 0,
-                       tmr_stream(stream), templates, units, U, C, total_rows, frags, ex);
+                       tmr_stream(stream), templates, units, U, C, total_rows, (int)(prec == TMR_PREC_BF16),
+                       frags, ex);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
 
-extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
+extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
+                                  int64_t total_rows, void *out, void *stream) {
+    return tmr_template_split_prec(templates, units, U, C, total_rows, TMR_PREC_F16X3, out, stream);
+}
+
+extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
                               const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
                               int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
                               float *work, float *out_absmax, const void *tmpl_split,
-                              int64_t total_rows, int algo, int min_k, void *stream) {
+                              int64_t total_rows, int algo, int min_k, int prec, void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
     TMR_REQUIRE(algo >= TMR_XCORR_AUTO && algo <= TMR_XCORR_MFMA);
+    TMR_REQUIRE(prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16);
     XArgs a;
     a.f = f;
     a.tmpl = templates;
@@ -946,7 +1009,7 @@ extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const 
     if (algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
     const bool use_mfma = algo == TMR_XCORR_MFMA || (algo == TMR_XCORR_AUTO && fits && min_k >= kMfmaMinK);
     if (use_mfma) {
-        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows);
+        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows, prec);
         if (rc != TMR_OK) return rc;
     } else {
         // row-tiled kernel when rows are 16-B aligned and templates fit its
@@ -981,6 +1044,16 @@ extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const 
         TMR_CHECK_LAUNCH();
     }
     return TMR_OK;
+}
+
+extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
+                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
+                              float *work, float *out_absmax, const void *tmpl_split,
+                              int64_t total_rows, int algo, int min_k, void *stream) {
+    return tmr_xcorr_prec(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
+                          relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, TMR_PREC_F16X3,
+                          stream);
 }
 
 extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,

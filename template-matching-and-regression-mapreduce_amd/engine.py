@@ -46,8 +46,9 @@ class PathConfig:
     decoder_num_layer: int = 1
     decoder_kernel_size: int = 3
     no_matcher: bool = False
-    # decoder-conv arithmetic: "fp32" (3-term fp16 split on 16-bit MFMA, the
-    # fp32 1e-5 contract), "bf16" (config C, 1e-2 contract) or "f16"
+    # decoder-conv and MFMA-correlation arithmetic: "fp32" (3-term fp16 split
+    # on 16-bit MFMA, the fp32 1e-5 contract), "bf16" (config C: one bf16
+    # term, 1e-2 contract) or "f16" (one scaled fp16 term)
     precision: str = "fp32"
 
     @classmethod
@@ -69,21 +70,26 @@ class PathConfig:
 # "auto" interpolates the regimes in log E, sums the per-unit costs of a
 # launch (linear in k in between) and runs the cheaper kernel: at E = 3 the
 # VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
-# crossover); at E = 16 MFMA wins from k = 9 on.
+# crossover); at E = 16 MFMA wins from k = 9 on.  Under the bf16 contract
+# (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr_prec) the MFMA
+# kernel wins from k = 7 at E = 3 (profiles/r02ab_*).
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
 _T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
     "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
     "mfma": (1.962, 2.577, 3.189, 3.755, 4.350, 4.796, 5.407, 5.987, 6.666, 10.969, 12.070, 13.200, 14.328, 15.542, 16.785, 17.876),
+    # one bf16 term (tmr_xcorr_prec, the bf16 contract), r02ab sweep
+    "mfma1": (1.813, 2.248, 2.600, 3.067, 3.494, 3.911, 4.257, 4.645, 5.000, 6.372, 6.713, 7.170, 7.636, 8.091, 8.623, 9.007),
 }
 _K192 = (3, 9, 15, 21, 31)
 _T192 = {  # ms per 128 units (E = 16) at 192^2, r02w sweep
     "valu": (2.539, 6.081, 13.025, 22.462, 51.697),
     "mfma": (3.192, 5.520, 7.462, 15.101, 22.257),
+    "mfma1": (3.093, 4.206, 6.205, 9.100, 12.010),
 }
 XCORR_COST = {
     a: (np.asarray(_T128[a]) / 192.0,
         np.interp(XCORR_COST_K, _K192, np.asarray(_T192[a]) / 128.0 / 2.25))
-    for a in ("valu", "mfma")
+    for a in ("valu", "mfma", "mfma1")
 }
 # A mixed-size MFMA launch stages every band with the LARGEST template's halo
 # rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
@@ -96,15 +102,18 @@ XCORR_COST = {
 XCORR_MFMA_MIX = 0.4
 
 
-def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool) -> str:
-    """The cheaper correlation kernel for a launch over units of these
-    template sizes (XCORR_COST model)."""
+def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool,
+                 one_term: bool = False) -> str:
+    """The cheaper correlation kernel ("valu" or "mfma") for a launch over
+    units of these template sizes (XCORR_COST model); one_term: the MFMA
+    kernel runs one 16-bit term (bf16 contract) instead of the 3-term split."""
     if not mfma_ok:
         return "valu"
     k = np.maximum(np.asarray(ht), np.asarray(wt)).astype(np.float64)
     lam = float(np.clip(np.log(max(units_per_image, 1.0) / 3.0) / np.log(16.0 / 3.0), 0.0, 1.0))
     cost = {}
-    for alg, (c3, c16) in XCORR_COST.items():
+    for alg, table in (("valu", "valu"), ("mfma", "mfma1" if one_term else "mfma")):
+        c3, c16 = XCORR_COST[table]
         per_k = (1.0 - lam) * c3 + lam * c16
         cost[alg] = float(np.interp(k, XCORR_COST_K, per_k).sum())
     if k.size and k.min() != k.max():
@@ -545,22 +554,26 @@ class TMREngine:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         min_k = int(min(units["ht"].min(), units["wt"].min()))
+        # MFMA operand precision: the fp32 path's 3-term split, or one bf16 /
+        # fp16 term under the bf16 contract (config C); the VALU kernels are fp32
+        pc = prec_code(cfg.precision)
         choice = self.xcorr_algo
         if choice == "auto":  # measured per-k cost model (XCORR_COST)
             fits = W % 32 == 0 and W <= 256 and mh <= 31 and mw <= 31 and (32 + mh // 2 * 2) * W <= 16384
-            choice = xcorr_choice(units["ht"], units["wt"], U / max(1, len(set(unit_image))), fits)
+            choice = xcorr_choice(units["ht"], units["wt"], U / max(1, len(set(unit_image))), fits,
+                                  one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
         tsplit = None
         if algo != XCORR_ALGOS["valu"] and tfl > 0:
-            # hi/lo fp16 operands of the MFMA correlation (per (unit, channel) scale)
+            # the MFMA correlation's template operands (per (unit, channel) scale)
             rows = host.tsplit_rows(units)
             tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
-            call("tmr_template_split", ptr(tmpl), ptr(units_d), U, C, rows, ptr(tsplit), stream())
-        call("tmr_xcorr_algo", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+            call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
+        call("tmr_xcorr_prec", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
              mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
              ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
-             rows if tsplit is not None else 0, algo, min_k, stream())
+             rows if tsplit is not None else 0, algo, min_k, pc, stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
