@@ -512,6 +512,17 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
 // XCD runs a contiguous range of (band, channel, image) blocks: neighbouring
 // bands' halo rows meet in that XCD's L2.
 constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
+// A-fragment prefetch distance in template rows.  One-term kernel: 4 rows
+// (its rows are 1/3 the MFMA work of the 3-term kernel's, so one row ahead
+// leaves the L2 latency exposed; measured at 128^2 E = 3, config-B mix: PF
+// 1/2/3/4/5/8 = 3.74/4.10/3.61/3.09/4.56/3.24 ms, profiles/r02ad_*, r02ae_*).
+// 3-term kernel: 1 row (PF 2/4: 5.85/5.28 vs 4.67 ms).
+#ifndef TMR_XCORR_PF1
+#define TMR_XCORR_PF1 4
+#endif
+#ifndef TMR_XCORR_PF3
+#define TMR_XCORR_PF3 1
+#endif
 constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -664,7 +675,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int PF = 1;  // prefetch distance (template rows; 2 and 3 measured equal, r02t)
+    constexpr int PF = SPLIT ? TMR_XCORR_PF3 : TMR_XCORR_PF1;  // prefetch distance (rows)
     V ah[PF][NK], al[PF][NK];
     auto afrag = [&](int i, int nk, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);

@@ -72,19 +72,19 @@ class PathConfig:
 # VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
 # crossover); at E = 16 MFMA wins from k = 9 on.  Under the bf16 contract
 # (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr_prec) the MFMA
-# kernel wins from k = 7 at E = 3 (profiles/r02ab_*).
+# kernel wins from k = 5 at E = 3 (profiles/r02af_*).
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
 _T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
     "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
     "mfma": (1.962, 2.577, 3.189, 3.755, 4.350, 4.796, 5.407, 5.987, 6.666, 10.969, 12.070, 13.200, 14.328, 15.542, 16.785, 17.876),
-    # one bf16 term (tmr_xcorr_prec, the bf16 contract), r02ab sweep
-    "mfma1": (1.813, 2.248, 2.600, 3.067, 3.494, 3.911, 4.257, 4.645, 5.000, 6.372, 6.713, 7.170, 7.636, 8.091, 8.623, 9.007),
+    # one bf16 term (tmr_xcorr_prec, the bf16 contract), r02af sweep (A prefetch 4 rows)
+    "mfma1": (1.875, 2.267, 2.280, 2.634, 2.972, 3.237, 3.465, 3.740, 4.002, 6.008, 6.330, 6.924, 7.386, 7.826, 8.118, 8.554),
 }
 _K192 = (3, 9, 15, 21, 31)
 _T192 = {  # ms per 128 units (E = 16) at 192^2, r02w sweep
     "valu": (2.539, 6.081, 13.025, 22.462, 51.697),
     "mfma": (3.192, 5.520, 7.462, 15.101, 22.257),
-    "mfma1": (3.093, 4.206, 6.205, 9.100, 12.010),
+    "mfma1": (2.919, 3.890, 4.632, 7.261, 9.791),
 }
 XCORR_COST = {
     a: (np.asarray(_T128[a]) / 192.0,
