@@ -262,6 +262,12 @@ int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, con
 #define TMR_SPLIT_TILED_INIT 2
 #define TMR_SPLIT_INIT_BCAST 4  /* acc_init is ONE slab shared by every unit
                                  * (e.g. the folded projection bias plane) */
+/* the tiled `out` (TMR_SPLIT_OUT_BF16) / tiled `acc_init` (TMR_SPLIT_INIT_BF16)
+ * hold bf16 values (round to nearest even) in the first half of the same
+ * allocation: one-term precisions only (the per-image fp half under the bf16
+ * contract; halves the heads launch's initial-value read) */
+#define TMR_SPLIT_OUT_BF16 8
+#define TMR_SPLIT_INIT_BF16 16
 int64_t tmr_split_acc_size(int U, int N, int H, int W);
 int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
                          int C1, int U, int H, int W, int ks, int prec, const void *wpack,

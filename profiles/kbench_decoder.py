@@ -76,6 +76,15 @@ def main():
             lambda p=p, pc=pc: call("tmr_split_conv_heads", None, 0, ptr(ui), ptr(xs[p]), C, U, H, W, 3,
                                     pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1, ptr(hw),
                                     ptr(acc0), ptr(part), 2, stream()), fl_d, terms)  # tiled acc0 (engine)
+        if p == "bf16":  # bf16 acc0 slab (TMR_SPLIT_INIT_BF16; values are garbage, timing only)
+            runs["split_bf16_heads_acc16"] = (
+                lambda p=p, pc=pc: call("tmr_split_conv_heads", None, 0, ptr(ui), ptr(xs[p]), C, U, H, W, 3,
+                                        pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1, ptr(hw),
+                                        ptr(acc0), ptr(part), 2 | 16, stream()), fl_d, terms)
+        runs[f"split_{p}_heads_noinit"] = (  # timing only: accumulators start at zero
+            lambda p=p, pc=pc: call("tmr_split_conv_heads", None, 0, ptr(ui), ptr(xs[p]), C, U, H, W, 3,
+                                    pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1, ptr(hw),
+                                    None, ptr(part), 0, stream()), fl_d, terms)
         runs[f"split_{p}_store"] = (
             lambda p=p, pc=pc: call("tmr_split_conv_store", ptr(xs[p]), C, None, None, 0, U, H, W, 3,
                                     pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 0, None,

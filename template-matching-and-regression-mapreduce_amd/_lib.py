@@ -43,6 +43,7 @@ TEMPLATE_PROTOTYPE = 1
 # decoder-conv precision modes of the split 16-bit-MFMA kernel (include/tmr.h)
 PREC_CODES = {"fp32": 0, "bf16": 1, "f16": 2}
 SPLIT_TILED_OUT, SPLIT_TILED_INIT, SPLIT_INIT_BCAST = 1, 2, 4
+SPLIT_OUT_BF16, SPLIT_INIT_BF16 = 8, 16  # one-term precisions: bf16 acc0 slabs
 # correlation kernel choice (tmr_xcorr_algo)
 XCORR_ALGOS = {"auto": 0, "valu": 1, "mfma": 2}
 

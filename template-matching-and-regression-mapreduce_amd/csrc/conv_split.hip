@@ -55,6 +55,7 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 b4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
@@ -82,6 +83,9 @@ constexpr int TW = 32;       // output cols per block
 #endif
 #ifndef TMR_SPLIT_ACC_NT  // non-temporal stores of the tiled acc0 (read back by a later launch; +0.4% config B)
 #define TMR_SPLIT_ACC_NT 1
+#endif
+#ifndef TMR_SPLIT_SPREAD  // tiled acc_init read 2 accumulators per chunk inside the main loop
+#define TMR_SPLIT_SPREAD 0
 #endif
 #ifndef TMR_SPLIT_NW
 #define TMR_SPLIT_NW 8
@@ -404,7 +408,36 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // accumulator register set is one contiguous KB per wave (no masking)
     const int islab = (a.flags & TMR_SPLIT_INIT_BCAST) ? 0 : img;  // acc_init slab
     const size_t tile_off = ((((size_t)islab * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW;
-    if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT)) {
+    // Spread initial values (tiled acc_init, >= NFR/2 chunks): the 32 KB per
+    // wave are read 2 KB per chunk (chunk c: accumulators 2c, 2c+1) and added
+    // at the chunk's end, instead of all before the main loop.  The blocks of
+    // a launch run in lockstep, so a prologue read is one chip-wide burst
+    // (48 units: 6.4 GB while no MFMA runs, 12% of the one-term kernel,
+    // profiles/r02ah_*); spread over the loop it hides under the MFMA stream.
+    // The loads are inline asm: the compiler does not track them, so it adds
+    // no vmcnt(0) before their use (that drained the next chunk's DMAs,
+    // r02ai); the step waits (counted vmcnt, in-order return) have landed
+    // them, as they are older than every DMA of the half-chunk.
+    constexpr int NFR = NIN * 8;  // f32x4 accumulators per lane
+    const bool spread = TMR_SPLIT_SPREAD && a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) &&
+                        !(a.flags & TMR_SPLIT_INIT_BF16) && 2 * NC >= NFR;
+    const float *abase = spread ? a.acc_init + tile_off : nullptr;  // this wave's 32 KB
+    if (spread) {
+#pragma unroll
+        for (int in = 0; in < NIN; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[in][jp][r] = 0.0f;
+    } else if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) && (a.flags & TMR_SPLIT_INIT_BF16)) {
+        // bf16 slab: the same 16-B-group index, 8 B per group
+        const b4 *ai = reinterpret_cast<const b4 *>(a.acc_init) + tile_off / 4 + lane;
+#pragma unroll
+        for (int in = 0; in < NIN; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp)
+                acc[in][jp] = __builtin_convertvector(ai[(in * 8 + jp) * 64], f32x4) * sxw;
+    } else if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT)) {
         const f32x4 *ai = reinterpret_cast<const f32x4 *>(a.acc_init + tile_off) + lane;
 #pragma unroll
         for (int in = 0; in < NIN; ++in)
@@ -465,6 +498,18 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     }
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
+        // spread acc_init: this chunk's two accumulators (zeros past the
+        // range), loaded at the start of its last half-chunk (F16X3: the lo
+        // one, whose A fragments take half the registers of the hi one)
+        f32x4 pre0 = {}, pre1 = {};
+        const bool sp = spread && 2 * c < NFR;  // wave-uniform
+        auto acc_load = [&]() {
+            if (sp) {
+                const int v0 = lane * 16 + 2 * c * 1024, v1 = v0 + 1024;
+                asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(pre0) : "v"(v0), "s"(abase) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(pre1) : "v"(v1), "s"(abase) : "memory");
+            }
+        };
         // one half-chunk; PART is a compile-time constant (F16X3: 0 = hi, 1 = lo)
         auto half_chunk = [&](auto part_c) {
             constexpr int part = decltype(part_c)::value;
@@ -600,14 +645,47 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 (step(std::integral_constant<int, SG>{}), ...);
             }(std::make_integer_sequence<int, SPC>{});
         };
+        if constexpr (HALVES == 1) acc_load();
         half_chunk(std::integral_constant<int, 0>{});
-        if constexpr (HALVES == 2) half_chunk(std::integral_constant<int, 1>{});
+        if constexpr (HALVES == 2) {
+            acc_load();
+            half_chunk(std::integral_constant<int, 1>{});
+        }
+        if (sp) {  // the step waits above have landed pre0/pre1
+#pragma unroll
+            for (int j = 0; j < NFR / 2; ++j)
+                if (j == c) {
+                    acc[(2 * j) / 8][(2 * j) % 8] += pre0 * sxw;
+                    acc[(2 * j + 1) / 8][(2 * j + 1) % 8] += pre1 * sxw;
+                }
+        }
     }
     // the last steps issued dummy DMAs (past the end) into LDS the epilogue reuses
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---------------- epilogue ----------------
+#if defined(TMR_SPLIT_EXP) && TMR_SPLIT_EXP == 1  // timing-only: no heads epilogue
+    if (EPI == 1) {
+        float s = 0.0f;
+#pragma unroll
+        for (int in = 0; in < NIN; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp) s += acc[in][jp][0] + acc[in][jp][1] + acc[in][jp][2] + acc[in][jp][3];
+        a.partials[(size_t)blockIdx.x * NTHREADS + tid] = s;
+        return;
+    }
+#endif
     const float inv = 1.0f / sxw;  // 2^-k: exact
+    if (EPI == 0 && (a.flags & TMR_SPLIT_TILED_OUT) && (a.flags & TMR_SPLIT_OUT_BF16)) {
+        b4 *o = reinterpret_cast<b4 *>(a.out) + ((((size_t)u * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW / 4 +
+                lane;
+#pragma unroll
+        for (int in = 0; in < NIN; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp)
+                __builtin_nontemporal_store(__builtin_convertvector(acc[in][jp] * inv, b4), o + (in * 8 + jp) * 64);
+        return;
+    }
     if (EPI == 0 && (a.flags & TMR_SPLIT_TILED_OUT)) {
         // raw conv result (scaled back) in the tiled acc layout of slab u: the
         // acc_init of a later launch; bias / activation are not applied here
@@ -637,65 +715,101 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     if (EPI == 1)
         for (int e = tid; e < BM * NHEAD; e += NTHREADS) shw[e] = a.headw[(size_t)nt * BM * NHEAD + e];
     __syncthreads();
-    float hs[8][NHEAD];
+    if constexpr (EPI == 0) {
 #pragma unroll
-    for (int jp = 0; jp < 8; ++jp)
+        for (int in = 0; in < NIN; ++in)
 #pragma unroll
-        for (int k = 0; k < NHEAD; ++k) hs[jp][k] = 0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const int nl = wn * 64 + in * 16 + 4 * kg + r;
+                const int n = nt * BM + nl;
+                const bool nin = n < a.N;
+                const float bn = sb[nl];
+#pragma unroll
+                for (int jp = 0; jp < 8; ++jp) {
+                    const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+                    float v = acc[in][jp][r] * inv + bn;
+                    if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
+                    if (nin && y < a.H && x < a.W) a.out[((size_t)u * a.N + n) * HW + (size_t)y * a.W + x] = v;
+                }
+            }
+        return;
+    }
+    // Heads: per pixel pair (jp = 2q, 2q+1) on v_pk_fma_f32.  acc * inv is
+    // exact (a power of two), so fma(acc, inv, bias) rounds once, like the
+    // separate multiply and add; LeakyReLU as max(v, 0.01 v) (= the select
+    // form for every v, incl. -0, inf and NaN).
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 hs2[4][NHEAD];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < NHEAD; ++k) hs2[q][k] = (f2){0.0f, 0.0f};
+    const f2 inv2 = {inv, inv};
 #pragma unroll
     for (int in = 0; in < NIN; ++in)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int nl = wn * 64 + in * 16 + 4 * kg + r;
-            const int n = nt * BM + nl;
-            const bool nin = n < a.N;
-            const float bn = sb[nl];
-            float hw[NHEAD];
-            if (EPI == 1) {
+            const f2 bn2 = {sb[nl], sb[nl]};
+            f2 hw2[NHEAD];
 #pragma unroll
-                for (int k = 0; k < NHEAD; ++k) hw[k] = shw[nl * NHEAD + k];
-            }
+            for (int k = 0; k < NHEAD; ++k) hw2[k] = (f2){shw[nl * NHEAD + k], shw[nl * NHEAD + k]};
 #pragma unroll
-            for (int jp = 0; jp < 8; ++jp) {
-                const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
-                float v = acc[in][jp][r] * inv + bn;
-                if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
-                if (EPI == 0) {
-                    if (nin && y < a.H && x < a.W) a.out[((size_t)u * a.N + n) * HW + (size_t)y * a.W + x] = v;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < NHEAD; ++k) hs[jp][k] = fmaf(v, hw[k], hs[jp][k]);
+            for (int q = 0; q < 4; ++q) {
+                f2 v = {acc[in][2 * q][r], acc[in][2 * q + 1][r]};
+                v = __builtin_elementwise_fma(v, inv2, bn2);
+                if (a.leaky) {
+                    const f2 m = v * (f2){0.01f, 0.01f};
+                    v = (f2){fmaxf(v.x, m.x), fmaxf(v.y, m.y)};
                 }
+#pragma unroll
+                for (int k = 0; k < NHEAD; ++k) hs2[q][k] = __builtin_elementwise_fma(v, hw2[k], hs2[q][k]);
             }
+            // keep the LDS reads of bias / head weights per row (hoisted, they
+            // would overlap the 128 live accumulators)
+            __builtin_amdgcn_sched_barrier(0);
         }
-    if (EPI == 1) {
-        // sum over the 4 lane groups (n rows), then over the two n-waves
+    // Sum over the 4 lane groups (rows of 16 lanes = n rows) by transpose-
+    // reduce: the 40 values X[j] (j = 2(5q + k) + (jp & 1)) pairwise through
+    // v_permlane16_swap (rows 0+1, 2+3), then v_permlane32_swap (halves):
+    // lane group kg ends with X[4p + kg], p = 0..9, summed as
+    // (x0 + x1) + (x2 + x3) -- the order of the xor-16 / xor-32 shuffles.
+    float X[40];
 #pragma unroll
-        for (int jp = 0; jp < 8; ++jp)
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int k = 0; k < NHEAD; ++k) {
-                hs[jp][k] += __shfl_xor(hs[jp][k], 16);
-                hs[jp][k] += __shfl_xor(hs[jp][k], 32);
-            }
-        __syncthreads();  // sb / shw reads are done before red is written
-        if (WNS == 2 && wn == 1 && kg == 0) {
-#pragma unroll
-            for (int jp = 0; jp < 8; ++jp)
-#pragma unroll
-                for (int k = 0; k < NHEAD; ++k) red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16] = hs[jp][k];
+        for (int k = 0; k < NHEAD; ++k) {
+            X[2 * (5 * q + k)] = hs2[q][k].x;
+            X[2 * (5 * q + k) + 1] = hs2[q][k].y;
         }
-        __syncthreads();
-        if (wn == 0 && kg == 0) {
+    float Y[20], Z[10];
 #pragma unroll
-            for (int jp = 0; jp < 8; ++jp) {
-                const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
-                if (y >= a.H || x >= a.W) continue;
+    for (int m = 0; m < 20; ++m) {
+        const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(X[2 * m]), __float_as_uint(X[2 * m + 1]),
+                                                         false, false);
+        Y[m] = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+    }
 #pragma unroll
-                for (int k = 0; k < NHEAD; ++k) {
-                    const float v = hs[jp][k] + (WNS == 2 ? red[((wpix * 8 + jp) * NHEAD + k) * 16 + l16] : 0.0f);
-                    a.partials[(((size_t)nt * NHEAD + k) * a.U + u) * HW + (size_t)y * a.W + x] = v;
-                }
-            }
+    for (int p = 0; p < 10; ++p) {
+        const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(Y[2 * p]), __float_as_uint(Y[2 * p + 1]),
+                                                         false, false);
+        Z[p] = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+    }
+    // then over the two n-waves (wn = 1 through LDS), every lane storing its 10
+    __syncthreads();  // sb / shw reads are done before red is written
+    if (WNS == 2 && wn == 1) {
+#pragma unroll
+        for (int p = 0; p < 10; ++p) red[((wpix * 10 + p) * 4 + kg) * 16 + l16] = Z[p];
+    }
+    __syncthreads();
+    if (wn == 0) {
+#pragma unroll
+        for (int p = 0; p < 10; ++p) {
+            const int j = 4 * p + kg, m = j >> 1, q = m / NHEAD, k = m - q * NHEAD;
+            const int jp = 2 * q + (j & 1);
+            const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+            const float v = Z[p] + (WNS == 2 ? red[((wpix * 10 + p) * 4 + kg) * 16 + l16] : 0.0f);
+            if (y < a.H && x < a.W) a.partials[(((size_t)nt * NHEAD + k) * a.U + u) * HW + (size_t)y * a.W + x] = v;
         }
     }
 }
@@ -899,6 +1013,10 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     TMR_REQUIRE(wpack && bias && U > 0 && H > 0 && W > 0 && N > 0 && C0 >= 0 && C1 >= 0);
     TMR_REQUIRE(C0 + C1 > 0 && (C0 == 0 || xp0) && (C1 == 0 || xp1));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || (wmax && xmax));
+    // bf16 slabs: one-term precisions, and only on a tiled out / tiled init
+    TMR_REQUIRE(!(flags & (TMR_SPLIT_OUT_BF16 | TMR_SPLIT_INIT_BF16)) || prec != TMR_PREC_F16X3);
+    TMR_REQUIRE(!(flags & TMR_SPLIT_OUT_BF16) || (flags & TMR_SPLIT_TILED_OUT));
+    TMR_REQUIRE(!(flags & TMR_SPLIT_INIT_BF16) || (flags & TMR_SPLIT_TILED_INIT));
     SArgs a = {};
     a.x0 = static_cast<const char *>(xp0);
     a.x1 = static_cast<const char *>(xp1);

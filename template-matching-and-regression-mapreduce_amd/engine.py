@@ -27,8 +27,8 @@ import numpy as np
 import torch
 
 from . import exp_table, host
-from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_TILED_INIT, SPLIT_TILED_OUT, XCORR_ALGOS,
-                   TMRError, call, load, ptr, require_gpu, stream)
+from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
+                   SPLIT_TILED_OUT, XCORR_ALGOS, TMRError, call, load, ptr, require_gpu, stream)
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
@@ -610,6 +610,12 @@ class TMREngine:
             if algo == "wino" and cfg.decoder_kernel_size != 3:
                 algo = "direct"
             wino, splitk = algo == "wino", algo == "split"
+            # the bf16 contract keeps the per-image fp half (acc0) in bf16:
+            # half the heads launch's initial-value read (a chip-wide burst
+            # before the first MFMA: 12% of the one-term kernel, r02ah;
+            # measured 10.49 -> 10.07 ms per 48 units, r02ak).  Not under
+            # "f16" (its 1e-3 contract: b 1.8e-3 with a bf16 acc0, r02ak).
+            acc16 = splitk and share and cfg.precision == "bf16"
             ks = cfg.decoder_kernel_size
             fold = splitk and cfg.fusion and self.fold_proj and feats is not None
             wp, bias, N, Cw, hw, hb, split, wbias = self._fused_decoders(C0 if share else 0, algo,
@@ -663,7 +669,7 @@ class TMREngine:
                 if splitk and acc0 is None:  # acc0 in the kernel's tiled accumulator layout (private)
                     acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
                                        dtype=torch.float32)
-                    fl = SPLIT_TILED_OUT
+                    fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0)
                     if bplane is not None:
                         fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST
                     call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
@@ -690,7 +696,7 @@ class TMREngine:
                 ev[0].record()
             s0 = ptr(src0) if src0 is not None else None
             a0 = ptr(acc0) if acc0 is not None else None
-            fl = SPLIT_TILED_INIT if a0 is not None else 0
+            fl = (SPLIT_TILED_INIT | (SPLIT_INIT_BF16 if acc16 else 0)) if a0 is not None else 0
             if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
                 a0, fl = ptr(bplane), SPLIT_TILED_INIT | SPLIT_INIT_BCAST
             if splitk:
