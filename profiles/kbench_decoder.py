@@ -90,6 +90,28 @@ def main():
                                     pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 0, None,
                                     ptr(out), 1, stream()), fl_d, terms)  # tiled out (engine)
         runs[f"split_{p}_xpack"] = (lambda p=p: pack_split_x(x, 3, p, xmax), 0.0, 0)
+    # the engine's layout: 3 units per image share the image's acc0 slab
+    ui3 = torch.div(torch.arange(U, device=dev, dtype=torch.int32), 3, rounding_mode="floor").to(torch.int32)
+    for p, terms, fl16 in (("fp32", 3, 0), ("bf16", 1, 16)):
+        pc = {"fp32": 0, "bf16": 1}[p]
+        runs[f"split_{p}_heads_e3"] = (
+            lambda p=p, pc=pc, fl16=fl16: call("tmr_split_conv_heads", None, 0, ptr(ui3), ptr(xs[p]), C, U, H, W,
+                                               3, pc, ptr(sp[p][0]), ptr(sp[p][1]), ptr(xmax), ptr(b), N, 1,
+                                               ptr(hw), ptr(acc0), ptr(part), 2 | fl16, stream()), fl_d, terms)
+    # the fp-half store at the engine's K = 256 (folded projection): with the
+    # broadcast bias-plane initial values (engine) and without
+    x256 = x[:, :256].contiguous()
+    xs256 = {p: pack_split_x(x256, 3, p, xmax) for p in ("fp32", "bf16")}
+    sp256 = {p: pack_split_w(w[:, :256].contiguous(), 256, p) for p in ("fp32", "bf16")}
+    fl_256 = fl_d / 2
+    for p, terms, fl16 in (("fp32", 3, 0), ("bf16", 1, 8)):
+        pc = {"fp32": 0, "bf16": 1}[p]
+        for tag, init, flags in (("bplane", acc0, 1 | 2 | 4 | fl16), ("noinit", None, 1 | fl16)):
+            runs[f"split_{p}_store256_{tag}"] = (
+                lambda p=p, pc=pc, init=init, flags=flags: call(
+                    "tmr_split_conv_store", ptr(xs256[p]), 256, None, None, 0, U, H, W, 3, pc, ptr(sp256[p][0]),
+                    ptr(sp256[p][1]), ptr(xmax), ptr(b), N, 0, ptr(init) if init is not None else None, ptr(out),
+                    flags, stream()), fl_256, terms)
     if os.environ.get("KB_ONLY"):
         runs = {k: v for k, v in runs.items() if k in os.environ["KB_ONLY"].split(",")}
     for name, spec in runs.items():
