@@ -87,6 +87,9 @@ constexpr int TW = 32;       // output cols per block
 #ifndef TMR_SPLIT_SPREAD  // tiled acc_init read 2 accumulators per chunk inside the main loop
 #define TMR_SPLIT_SPREAD 0
 #endif
+#ifndef TMR_SPLIT_HOIST_HOFF  // halo DMA per-lane offsets computed once (VGPRs) instead of per DMA
+#define TMR_SPLIT_HOIST_HOFF 1
+#endif
 #ifndef TMR_SPLIT_NW
 #define TMR_SPLIT_NW 8
 #endif
@@ -326,7 +329,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // rather than held in registers through the main loop.
     auto hoff = [&](int m) -> int {
         int ln = lane;
+#if !TMR_SPLIT_HOIST_HOFF
         asm volatile("" : "+v"(ln));  // opaque: keeps LICM from hoisting (and spilling) the offsets
+#endif
         const int e = (wave + NWAVES * m) * 64 + ln;
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
