@@ -281,6 +281,68 @@ def test_split_conv_scales_and_two_sources(scale):
     assert normwise(got[1], ref[1]) <= TOL
 
 
+def test_split_acc_slab_bf16():
+    """The bf16 per-image fp-half slab of the bf16 contract (TMR_SPLIT_OUT_BF16
+    on the store, TMR_SPLIT_INIT_BF16 on the heads launch): heads partials from
+    a bf16 slab vs an fp32 slab of the same store (bf16 rounding of the
+    initial values only), and vs the unsplit fp64 reference within the bf16
+    contract; the flags are refused under the fp32 3-term split and without a
+    tiled buffer."""
+    from tmr_amd._lib import (PREC_CODES, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
+                              SPLIT_TILED_OUT, call, load, ptr, stream)
+    from tmr_amd.engine import absmax, pack_split_w, pack_split_x
+    torch.manual_seed(5)
+    B, U, C0, C1, N, H, W = 2, 3, 40, 48, 136, 19, 37
+    x0, x1 = torch.randn(B, C0, H, W), torch.randn(U, C1, H, W)
+    ui = np.array([1, 0, 1], np.int32)
+    w = torch.randn(N, C0 + C1, 3, 3) * 0.02
+    bias = torch.randn(N) * 0.1
+    hw = torch.zeros(((N + 127) // 128) * 128, 5)
+    hw[:N] = torch.randn(N, 5)
+    xcat = torch.cat([x0[torch.from_numpy(ui).long()], x1], 1)
+    act = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(xcat.double(), w.double(),
+                                                                    bias.double(), padding=1), 0.01)
+    ref = torch.einsum("unhw,nj->ujhw", act, hw[:N].double()).numpy()
+    d = {k: cuda(v) for k, v in dict(x0=x0, x1=x1, w0=w[:, :C0].contiguous(), w1=w[:, C0:].contiguous(),
+                                     b=bias, hw=hw).items()}
+    zero = torch.zeros(N, device=DEV)
+    uid = cuda(torch.from_numpy(ui))
+    pc = PREC_CODES["bf16"]
+    wp0, wm0 = pack_split_w(d["w0"], C0, "bf16")
+    wp1, wm1 = pack_split_w(d["w1"], 0, "bf16")
+    xm0, xm1 = absmax(d["x0"]), absmax(d["x1"])
+    xp0, xp1 = pack_split_x(d["x0"], 3, "bf16", xm0), pack_split_x(d["x1"], 3, "bf16", xm1)
+    slabs = {}
+    for tag, fl in (("fp32", 0), ("bf16", SPLIT_OUT_BF16)):
+        slabs[tag] = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=DEV)
+        call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0),
+             ptr(xm0), ptr(zero), N, 0, None, ptr(slabs[tag]), SPLIT_TILED_OUT | fl, stream())
+    got = {}
+    for tag, fl in (("fp32", 0), ("bf16", SPLIT_INIT_BF16)):
+        part = torch.empty(load().tmr_heads_partials_size(N, U, H, W), device=DEV)
+        call("tmr_split_conv_heads", None, 0, ptr(uid), ptr(xp1), C1, U, H, W, 3, pc, ptr(wp1), ptr(wm1),
+             ptr(xm1), ptr(d["b"]), N, 1, ptr(d["hw"]), ptr(slabs[tag]), ptr(part), SPLIT_TILED_INIT | fl,
+             stream())
+        o, bb = torch.empty((U, 1, H, W), device=DEV), torch.empty((U, 4, H, W), device=DEV)
+        call("tmr_heads_reduce", ptr(part), N, 128, U, H, W, ptr(torch.zeros(5, device=DEV)), ptr(o), ptr(bb),
+             stream())
+        torch.cuda.synchronize()
+        got[tag] = np.concatenate([bb.cpu().numpy(), o.cpu().numpy()], 1)
+    e_slab = normwise(got["bf16"], got["fp32"])
+    e_ref = max(normwise(got["bf16"][u], ref[u]) for u in range(U))
+    print(f"bf16 slab vs fp32 slab {e_slab:.2e}, vs fp64 reference {e_ref:.2e}")
+    assert 0.0 < e_slab <= 1e-2 and e_ref <= SPLIT_TOL["bf16"]
+    out = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=DEV)
+    wpf, wmf = pack_split_w(d["w0"], C0, "fp32")
+    with pytest.raises(tmr_amd.TMRError):  # bf16 slabs are a one-term-precision layout
+        call("tmr_split_conv_store", ptr(pack_split_x(d["x0"], 3, "fp32", xm0)), C0, None, None, 0, B, H, W, 3,
+             PREC_CODES["fp32"], ptr(wpf), ptr(wmf), ptr(xm0), ptr(zero), N, 0, None, ptr(out),
+             SPLIT_TILED_OUT | SPLIT_OUT_BF16, stream())
+    with pytest.raises(tmr_amd.TMRError):  # OUT_BF16 needs the tiled output
+        call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0), ptr(xm0),
+             ptr(zero), N, 0, None, ptr(out), SPLIT_OUT_BF16, stream())
+
+
 def test_wino_matches_direct_decoders():
     B, E = 2, 2
     P = synth.reference_state_dict(4, cin=64, emb=96, obj_bias=-0.3)
