@@ -57,17 +57,13 @@ typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 b4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// Register-staged operand loads (Geo::wcount: buffer_load_dwordx4 to VGPRs,
-// ds_write_b128 a step later, two steps of lookahead) instead of LDS-DMA.
-// Correct (the GPU parity suite passes with it) but measured slower at config
-// B: heads 29.93 vs 28.86 ms per 48 units, 427 vs 436 images/s
-// (profiles/r02p_*) -- the ds_write data transfer and the lgkmcnt waits it
-// adds to the fragment reads cost more than the LDS-DMA issue it saves.
-#ifndef TMR_SPLIT_RS
-#define TMR_SPLIT_RS 0
-#endif
+// Measured and dropped (code in git history): register-staged operand loads
+// (buffer_load + ds_write instead of LDS-DMA; 3.7% slower, profiles/r02p_*),
+// initial values read inside the main loop (slower: a load issued in a step
+// is forced by that step's in-order vmcnt wait; profiles/r02ai, r02aj), the
+// next step's first B fragments read before the step barrier (4% slower,
+// r02an), wave priority over the MFMA stream (no change, r02av).
 
 constexpr int BM = 128;      // output channels per block
 constexpr int TH = 16;       // output rows per block
@@ -83,9 +79,6 @@ constexpr int TW = 32;       // output cols per block
 #endif
 #ifndef TMR_SPLIT_ACC_NT  // non-temporal stores of the tiled acc0 (read back by a later launch; +0.4% config B)
 #define TMR_SPLIT_ACC_NT 1
-#endif
-#ifndef TMR_SPLIT_SPREAD  // tiled acc_init read 2 accumulators per chunk inside the main loop
-#define TMR_SPLIT_SPREAD 0
 #endif
 #ifndef TMR_SPLIT_HOIST_HOFF  // halo DMA per-lane offsets computed once (VGPRs) instead of per DMA
 #define TMR_SPLIT_HOIST_HOFF 1
@@ -252,22 +245,6 @@ struct Geo {
         }
         return n;
     }
-    // Register-staged operand path (RS; D == 1 geometries with SPC >= 2): the
-    // weights of step g+2 are loaded into VGPRs during step g and written to
-    // LDS during step g+1 (into the buffer step g read), so an LDS buffer pair
-    // gives two steps of load latency; the next half-chunk's halo is loaded
-    // during steps 0..SPC-2 and written one step later.  A buffer_load +
-    // ds_write_b128 pair issues in a fraction of an LDS-DMA's cost.
-    static constexpr int wcount(int sgx, int part, int halves) {  // pieces per wave, step sg+x
-        return (T - (sgx % SPC) * TPS < TPS ? T - (sgx % SPC) * TPS : TPS) * ipt(lo_of(sgx, part, halves)) /
-               NWAVES;
-    }
-    static constexpr int QL = SPC >= 2 ? (MPW + SPC - 2) / (SPC - 1) : MPW;  // halo loads per step
-    static constexpr int hl(int sg) {
-        return sg > SPC - 2 ? 0 : MPW - sg * QL < QL ? (MPW - sg * QL > 0 ? MPW - sg * QL : 0) : QL;
-    }
-    static constexpr int hs(int sg) { return sg == 0 ? 0 : hl(sg - 1); }
-    static constexpr int MAXW = TPS * NPLW * 2 / NWAVES;  // weight pieces per wave of a hi step
     static_assert(fits(TPS, NWB), "LDS");
 };
 
@@ -357,15 +334,6 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         char *dst = Hs + (hc & 1) * HB;
         buffer_lds16(s0 ? xr0 : xr1, (lds_ptr_t)(dst + (wave + NWAVES * m) * 1024), hoff(m), soff);
     };
-    // the same piece through a VGPR quad (RS path): load, and write to LDS later
-    auto halo_load = [&](int hc, int m) -> v4u {
-        const bool s0 = hc < h0;
-        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;
-        return __builtin_amdgcn_raw_buffer_load_b128(s0 ? xr0 : xr1, hoff(m), soff, 0);
-    };
-    auto halo_store = [&](int hc, int m, v4u v) {
-        *reinterpret_cast<v4u *>(Hs + (hc & 1) * HB + (wave + NWAVES * m) * 1024 + lane * 16) = v;
-    };
     // weights of flat step g: half-chunk g / SPC (hi: wh and wl planes, lo:
     // wh only), taps TPS*(g % SPC)...; instruction i of the step = tap i/IPT,
     // plane (i%IPT)/2, channels 64*((i%IPT)&1) + lane: 1 KB contiguous in the
@@ -395,12 +363,6 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     auto w_dma1 = [&](int g, int ipt, int m) {
         buffer_lds16(wr, (lds_ptr_t)w_dst(g, ipt, m), wlane, w_src(g, ipt, m));
     };
-    auto w_load = [&](int g, int ipt, int m) -> v4u {
-        return __builtin_amdgcn_raw_buffer_load_b128(wr, wlane, w_src(g, ipt, m), 0);
-    };
-    auto w_store = [&](int g, int ipt, int m, v4u v) {
-        *reinterpret_cast<v4u *>(w_dst(g, ipt, m) + lane * 16) = v;
-    };
 
     // accumulators start at acc_init (scaled into the accumulator's units by
     // the exact power of two s_x s_w); masked elements read a clamped legal
@@ -409,32 +371,15 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     const float sxw = PR::SCALED ? split_scale(a.xmax) * split_scale(a.wmax) : 1.0f;
     const int HW = a.H * a.W;
     f32x4 acc[NIN][8];
-    // tiled acc layout: [slab][nt][mt][wave][in*8+jp][lane][4] fp32, i.e. each
-    // accumulator register set is one contiguous KB per wave (no masking)
+    // tiled acc layout: [slab][nt][mt][wave][in*8+jp][lane][4] fp32 (bf16
+    // slabs: 8 B per 16-B group index), i.e. each accumulator register set is
+    // one contiguous KB per wave (no masking).  Read before the main loop: the
+    // blocks run in lockstep, so this is a chip-wide burst while no MFMA runs
+    // (12% of the one-term kernel with fp32 slabs, profiles/r02ah_*; halved
+    // by the bf16 slab of the bf16 contract)
     const int islab = (a.flags & TMR_SPLIT_INIT_BCAST) ? 0 : img;  // acc_init slab
     const size_t tile_off = ((((size_t)islab * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW;
-    // Spread initial values (tiled acc_init, >= NFR/2 chunks): the 32 KB per
-    // wave are read 2 KB per chunk (chunk c: accumulators 2c, 2c+1) and added
-    // at the chunk's end, instead of all before the main loop.  The blocks of
-    // a launch run in lockstep, so a prologue read is one chip-wide burst
-    // (48 units: 6.4 GB while no MFMA runs, 12% of the one-term kernel,
-    // profiles/r02ah_*); spread over the loop it hides under the MFMA stream.
-    // The loads are inline asm: the compiler does not track them, so it adds
-    // no vmcnt(0) before their use (that drained the next chunk's DMAs,
-    // r02ai); the step waits (counted vmcnt, in-order return) have landed
-    // them, as they are older than every DMA of the half-chunk.
-    constexpr int NFR = NIN * 8;  // f32x4 accumulators per lane
-    const bool spread = TMR_SPLIT_SPREAD && a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) &&
-                        !(a.flags & TMR_SPLIT_INIT_BF16) && 2 * NC >= NFR;
-    const float *abase = spread ? a.acc_init + tile_off : nullptr;  // this wave's 32 KB
-    if (spread) {
-#pragma unroll
-        for (int in = 0; in < NIN; ++in)
-#pragma unroll
-            for (int jp = 0; jp < 8; ++jp)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[in][jp][r] = 0.0f;
-    } else if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) && (a.flags & TMR_SPLIT_INIT_BF16)) {
+    if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) && (a.flags & TMR_SPLIT_INIT_BF16)) {
         // bf16 slab: the same 16-B-group index, 8 B per group
         const b4 *ai = reinterpret_cast<const b4 *>(a.acc_init) + tile_off / 4 + lane;
 #pragma unroll
@@ -490,31 +435,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
         for (int m = 0; m < nt0; ++m) w_dma1(g0, ipt_of(lo0), m);
     }
-    constexpr bool RS = TMR_SPLIT_RS && D == 1 && SPC >= 2;
-    v4u rw[G::MAXW > 0 ? G::MAXW : 1], rh[G::QL > 0 ? G::QL : 1];  // RS: pieces in flight
-    if constexpr (RS) {
-        // the weights of step 1 into VGPRs (step 0 writes them to LDS)
-        constexpr int n1 = G::wcount(1, 0, HALVES);
-#pragma unroll
-        for (int m = 0; m < n1; ++m) rw[m] = w_load(1, ipt_of(G::lo_of(1, 0, HALVES)), m);
-        wait_vmcnt(n1);  // the DMAs above (older) have landed
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int c = 0; c < NC; ++c) {
-        // spread acc_init: this chunk's two accumulators (zeros past the
-        // range), loaded at the start of its last half-chunk (F16X3: the lo
-        // one, whose A fragments take half the registers of the hi one)
-        f32x4 pre0 = {}, pre1 = {};
-        const bool sp = spread && 2 * c < NFR;  // wave-uniform
-        auto acc_load = [&]() {
-            if (sp) {
-                const int v0 = lane * 16 + 2 * c * 1024, v1 = v0 + 1024;
-                asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(pre0) : "v"(v0), "s"(abase) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(pre1) : "v"(v1), "s"(abase) : "memory");
-            }
-        };
         // one half-chunk; PART is a compile-time constant (F16X3: 0 = hi, 1 = lo)
         auto half_chunk = [&](auto part_c) {
             constexpr int part = decltype(part_c)::value;
@@ -535,31 +458,13 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 constexpr int nh = G::nh(sg);
                 constexpr bool loD = G::lo_of(sg + D, part, HALVES);
                 constexpr int nw = G::nw(sg, part, HALVES);
-                // RS: first write the pieces loaded during the previous step
-                // (halo slice of hc+1, weights of g+1), then load the next
-                // ones (halo slice, weights of g+2) into the freed VGPRs
-                constexpr int nsh = RS ? G::hs(sg) : 0, nsw = RS ? G::wcount(sg + 1, part, HALVES) : 0;
-                constexpr int nlh = RS ? G::hl(sg) : 0, nlw = RS ? G::wcount(sg + 2, part, HALVES) : 0;
-                constexpr bool lo1 = G::lo_of(sg + 1, part, HALVES), lo2 = G::lo_of(sg + 2, part, HALVES);
-                constexpr int NSLOT = RS ? nsh + nsw + nlh + nlw : nh + nw;
+                constexpr int NSLOT = nh + nw;
                 auto dma_slot = [&](int k) {  // slot k of this step (k < NSLOT)
-                    if constexpr (RS) {
-                        if (k < nsh)
-                            halo_store(hc + 1, (sg - 1) * G::QL + k, rh[k]);
-                        else if (k < nsh + nsw)
-                            w_store(g + 1, ipt_of(lo1), k - nsh, rw[k - nsh]);
-                        else if (k < nsh + nsw + nlh)
-                            rh[k - nsh - nsw] = halo_load(hc + 1, sg * G::QL + (k - nsh - nsw));
-                        else
-                            rw[k - nsh - nsw - nlh] = w_load(g + 2, ipt_of(lo2), k - nsh - nsw - nlh);
-                    } else {
-                        if (k < nh)
-                            halo_dma1(hc + 1, sg * Q + k);
-                        else
-                            w_dma1(g + D, ipt_of(loD), k - nh);
-                    }
+                    if (k < nh)
+                        halo_dma1(hc + 1, sg * Q + k);
+                    else
+                        w_dma1(g + D, ipt_of(loD), k - nh);
                 };
-                auto slot_kind = [&](int k) { return RS && k < nsh + nsw ? 0x200 : 0x020; };  // DS write / VMEM
                 const char *wl = Ws + (g % NWB) * WB;
                 // Register pipeline: the A (weight) fragments of a tap are
                 // read during the previous tap of the step, the B (halo)
@@ -619,12 +524,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                         else if (nr == 1)
                             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                        if (dm) {
-                            if (slot_kind(k) == 0x200)
-                                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                            else
-                                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-                        }
+                        if (dm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
                     }
                 }
@@ -635,12 +535,9 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                     if (k >= ntap * 8 - 1 && k < NSLOT) dma_slot(k);
                 __builtin_amdgcn_sched_barrier(0);
                 // the next step needs W(g+1) and, after a half-chunk's last
-                // step, the whole halo of hc+1: RS -- this step's LDS writes
-                // done; DMA -- leave only younger DMAs in flight (in-order
-                // completion; halo issued before weights)
-                if constexpr (RS)
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                else if (D == 1)
+                // step, the whole halo of hc+1: leave only younger DMAs in
+                // flight (in-order completion; halo issued before weights)
+                if constexpr (D == 1)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 else
                     wait_vmcnt(G::allowed(sg, part, HALVES));
@@ -650,36 +547,13 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 (step(std::integral_constant<int, SG>{}), ...);
             }(std::make_integer_sequence<int, SPC>{});
         };
-        if constexpr (HALVES == 1) acc_load();
         half_chunk(std::integral_constant<int, 0>{});
-        if constexpr (HALVES == 2) {
-            acc_load();
-            half_chunk(std::integral_constant<int, 1>{});
-        }
-        if (sp) {  // the step waits above have landed pre0/pre1
-#pragma unroll
-            for (int j = 0; j < NFR / 2; ++j)
-                if (j == c) {
-                    acc[(2 * j) / 8][(2 * j) % 8] += pre0 * sxw;
-                    acc[(2 * j + 1) / 8][(2 * j + 1) % 8] += pre1 * sxw;
-                }
-        }
+        if constexpr (HALVES == 2) half_chunk(std::integral_constant<int, 1>{});
     }
     // the last steps issued dummy DMAs (past the end) into LDS the epilogue reuses
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---------------- epilogue ----------------
-#if defined(TMR_SPLIT_EXP) && TMR_SPLIT_EXP == 1  // timing-only: no heads epilogue
-    if (EPI == 1) {
-        float s = 0.0f;
-#pragma unroll
-        for (int in = 0; in < NIN; ++in)
-#pragma unroll
-            for (int jp = 0; jp < 8; ++jp) s += acc[in][jp][0] + acc[in][jp][1] + acc[in][jp][2] + acc[in][jp][3];
-        a.partials[(size_t)blockIdx.x * NTHREADS + tid] = s;
-        return;
-    }
-#endif
     const float inv = 1.0f / sxw;  // 2^-k: exact
     if (EPI == 0 && (a.flags & TMR_SPLIT_TILED_OUT) && (a.flags & TMR_SPLIT_OUT_BF16)) {
         b4 *o = reinterpret_cast<b4 *>(a.out) + ((((size_t)u * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW / 4 +
