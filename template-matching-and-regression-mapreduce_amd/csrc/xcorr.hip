@@ -355,8 +355,10 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
     }
 }
 
-// One unit's band for the rows kernel in TY x TX lane tiles.
-template <int TY, int TX>
+// One unit's band for the rows kernel in TY x TX lane tiles; width
+// specialisations up to MAXW (the launch's widest template: a kernel without
+// the 17..31 cases holds fewer scalar registers live and spills fewer).
+template <int TY, int TX, int MAXW>
 __device__ __forceinline__ void rows_unit(const float *xs, int WS, int W, int yb0, int yb1, int hg, int h,
                                           int w, int ph, int pw, int Ho, int Wo,
                                           const float *__restrict__ tc, float denom, float rden, float sc,
@@ -374,7 +376,7 @@ __device__ __forceinline__ void rows_unit(const float *xs, int WS, int W, int yb
         // tiles wholly in the border rows or columns only store zeros
         const bool live = y0 + TY > ph && y0 < ph + Ho && c0 + TX > pw && c0 < pw + Wo;
         if (live) switch (w) {
-#define TMR_W(K) case K: corr_tile<K, TY, TX>(xs, WS, lrow0, lcol0, tc, h, pa); break;
+#define TMR_W(K) case K: if constexpr (K <= MAXW) corr_tile<K, TY, TX>(xs, WS, lrow0, lcol0, tc, h, pa); break;
             TMR_W(1) TMR_W(3) TMR_W(5) TMR_W(7) TMR_W(9) TMR_W(11) TMR_W(13) TMR_W(15)
             TMR_W(17) TMR_W(19) TMR_W(21) TMR_W(23) TMR_W(25) TMR_W(27) TMR_W(29) TMR_W(31)
 #undef TMR_W
@@ -406,6 +408,7 @@ __device__ __forceinline__ void rows_unit(const float *xs, int WS, int W, int yb
     }
 }
 
+template <int MAXW>
 __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__restrict__ tmpl,
                                                        float *__restrict__ outp,
                                                        const tmr_unit_t *__restrict__ units) {
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
         // 4x4 tiles: one 16-B store per lane row (1 KB per wave row).  2x8
         // tiles (twice the FMAs per scalar tap-row load) measured 5.1 vs 5.5
         // ms at k = 9 but 10.4 vs 7.4 at k = 11 and 16.4 vs 11.4 at k = 15.
-        rows_unit<4, 4>(xs, WS, W, yb0, yb1, hg, h, w, ph, pw, Ho, Wo, tc, denom, rden, sc, op, rp, vmax);
+        rows_unit<4, 4, MAXW>(xs, WS, W, yb0, yb1, hg, h, w, ph, pw, Ho, Wo, tc, denom, rden, sc, op, rp, vmax);
     }
     if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
         for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
@@ -1036,13 +1039,17 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
         a.HG = max_ht / 2;
         const size_t lds = rows ? (size_t)a.LR * WS * sizeof(float)
                                 : ((size_t)a.LR * W + XSLACK) * sizeof(float);
-        const void *kfn = rows ? (const void *)xcorr_rows_kernel : (const void *)xcorr_kernel;
+        const bool narrow = max_wt <= 15;
+        const void *kfn = !rows ? (const void *)xcorr_kernel
+                          : narrow ? (const void *)xcorr_rows_kernel<15> : (const void *)xcorr_rows_kernel<31>;
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return TMR_E_HIP;
         dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
-        if (rows)
-            hipLaunchKernelGGL(xcorr_rows_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
+        if (rows && narrow)
+            hipLaunchKernelGGL(xcorr_rows_kernel<15>, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
+        else if (rows)
+            hipLaunchKernelGGL(xcorr_rows_kernel<31>, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
         else
             hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
         TMR_CHECK_LAUNCH();
