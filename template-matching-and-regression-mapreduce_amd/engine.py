@@ -446,11 +446,17 @@ class TMREngine:
             plane = torch.empty(load().tmr_split_acc_size(1, N, H, W), device=dev, dtype=torch.float32)
             zero = torch.zeros(N, device=dev, dtype=torch.float32)
             call("tmr_split_conv_store", ptr(xp), 1, None, None, 0, 1, H, W, ks, prec_code(prec),
-                 ptr(wp), ptr(wmax), ptr(one), ptr(zero), N, 0, None, ptr(plane), SPLIT_TILED_OUT,
-                 stream())
+                 ptr(wp), ptr(wmax), ptr(one), ptr(zero), N, 0, None, ptr(plane),
+                 SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if self._plane16() else 0), stream())
             return plane
 
         return self._cache.get(f"bias_plane_{H}x{W}_{prec}", [wbias], build)
+
+    def _plane16(self) -> bool:
+        """The bias plane slab is kept in bf16 under the bf16 contract (its
+        broadcast read is the fp-half store's initial-value burst: 9% of that
+        launch in fp32, r02am)."""
+        return self.cfg.precision == "bf16"
 
     def _conv(self, name: str, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool):
         """One nn.Conv2d (+ LeakyReLU) of the general-depth stack on the
@@ -671,7 +677,7 @@ class TMREngine:
                                        dtype=torch.float32)
                     fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0)
                     if bplane is not None:
-                        fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST
+                        fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
                     call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
                          ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0,
                          ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
@@ -698,7 +704,8 @@ class TMREngine:
             a0 = ptr(acc0) if acc0 is not None else None
             fl = (SPLIT_TILED_INIT | (SPLIT_INIT_BF16 if acc16 else 0)) if a0 is not None else 0
             if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
-                a0, fl = ptr(bplane), SPLIT_TILED_INIT | SPLIT_INIT_BCAST
+                a0 = ptr(bplane)
+                fl = SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
             if splitk:
                 call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                      U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
