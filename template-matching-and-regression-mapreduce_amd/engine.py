@@ -498,22 +498,27 @@ class TMREngine:
         up = self.cfg.feature_upsample
         H, W = (2 * Hin, 2 * Win) if up else (Hin, Win)
         if self.decoder_algo == "split":
-            # 1x1 conv on the split kernel (always the fp32-grade 3-term split:
-            # fp feeds the templates and the correlation) from records of
-            # up2x(f) packed straight from the SAM features; f[0] (the module
-            # API output, matching_net.py:81) by the upsample kernel alone
+            # 1x1 conv on the split kernel from records of up2x(f) packed
+            # straight from the SAM features; f[0] (the module API output,
+            # matching_net.py:81) by the upsample kernel alone.  The fp32-grade
+            # 3-term split except under the bf16 contract, where fp feeds only
+            # one-term bf16 arithmetic downstream (the correlation and the
+            # decoders' f_TM half; the fp half is folded from the features):
+            # one bf16 term here too (forward error measured within 1e-2)
+            pprec = "bf16" if self.cfg.precision == "bf16" else "fp32"
+            pcode = prec_code(pprec)
             pw, pb = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
             N, Cw = pw.shape[0], pw.shape[1]
             if Cw != Cin:
                 raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
-            wp, wmax = self._cache.get("proj_split", [pw], lambda: pack_split_w(pw, Cin, "fp32"))
+            wp, wmax = self._cache.get(f"proj_split_{pprec}", [pw], lambda: pack_split_w(pw, Cin, pprec))
             xmax = self._feat_absmax(feats)
-            n = load().tmr_split_xpack_size(B, Cin, H, W, 1, 0)
+            n = load().tmr_split_xpack_size(B, Cin, H, W, 1, pcode)
             xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
-            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up), 0, 1, 0, ptr(xmax),
+            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up), 0, 1, pcode, ptr(xmax),
                  ptr(xp), stream())
             fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
-            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, H, W, 1, 0, ptr(wp),
+            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, H, W, 1, pcode, ptr(wp),
                  ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fp),
                  0, stream())
             f0 = None
