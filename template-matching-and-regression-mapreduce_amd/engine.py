@@ -340,6 +340,9 @@ class TMREngine:
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
+        # split path: input_proj at the SAM features' size, then bilinear x2
+        # (the same linear map as input_proj(up2x(f)), 4x fewer MFMAs)
+        self.proj_before_upsample = True
         self._fp_memo = None
         self._acc0_memo = None
         self.last_decoder_flops = 0.0
@@ -513,14 +516,27 @@ class TMREngine:
                 raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
             wp, wmax = self._cache.get(f"proj_split_{pprec}", [pw], lambda: pack_split_w(pw, Cin, pprec))
             xmax = self._feat_absmax(feats)
-            n = load().tmr_split_xpack_size(B, Cin, H, W, 1, pcode)
+            # the 1x1 projection commutes with the bilinear x2 (both linear;
+            # the interpolation weights of each output sum to 1, so the bias
+            # passes through): project at the features' size, then upsample
+            # the projection -- a quarter of the MFMA work
+            # (input_proj(up2x(f)) and up2x(input_proj(f)) differ in fp32
+            # rounding only)
+            early = up and self.proj_before_upsample
+            Hq, Wq = (Hin, Win) if early else (H, W)
+            n = load().tmr_split_xpack_size(B, Cin, Hq, Wq, 1, pcode)
             xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
-            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up), 0, 1, pcode, ptr(xmax),
-                 ptr(xp), stream())
-            fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
-            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, H, W, 1, pcode, ptr(wp),
-                 ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fp),
+            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up and not early), 0, 1, pcode,
+                 ptr(xmax), ptr(xp), stream())
+            fq = torch.empty((B, N, Hq, Wq), device=feats.device, dtype=torch.float32)
+            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
+                 ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
                  0, stream())
+            if early:
+                fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
+                call("tmr_upsample2x", ptr(fq), B * N, Hin, Win, ptr(fp), stream())
+            else:
+                fp = fq
             f0 = None
             if want_f0:
                 if up:
