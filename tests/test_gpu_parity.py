@@ -281,6 +281,33 @@ def test_split_conv_scales_and_two_sources(scale):
     assert normwise(got[1], ref[1]) <= TOL
 
 
+@pytest.mark.parametrize("Hin,Win", [(64, 64), (33, 47), (7, 5), (40, 70)])
+def test_upsample2x_tiled_and_projection_order(Hin, Win):
+    """tmr_upsample2x (LDS-tiled, 32x128 output tiles) bit-exact against the C
+    restatement at tile-edge and W % 4 != 0 sizes; the engine's projection
+    input_proj at the features' size then up2x (default) and input_proj on
+    up2x(f) (proj_before_upsample=False) both within the fp32 contract of
+    ATen's conv2d(interpolate(f)) (matching_net.py:50-51,56)."""
+    from tmr_amd._lib import call, ptr, stream
+    torch.manual_seed(Hin * 100 + Win)
+    C = 24
+    f = torch.randn(2, C, Hin, Win)
+    fd = cuda(f)
+    out = torch.empty((2, C, 2 * Hin, 2 * Win), device=DEV)
+    call("tmr_upsample2x", ptr(fd), 2 * C, Hin, Win, ptr(out), stream())
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), np.stack([oracle.upsample2x(x) for x in f.numpy()]))
+    P = synth.reference_state_dict(3, cin=C, emb=40)
+    ref = torch.nn.functional.conv2d(
+        torch.nn.functional.interpolate(f, scale_factor=2, mode="bilinear", align_corners=False),
+        P["input_proj.0.weight"], P["input_proj.0.bias"])
+    for early in (True, False):
+        eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=40))
+        eng.proj_before_upsample = early
+        fp, _ = eng.project(fd)
+        assert normwise(fp.cpu().numpy(), ref.numpy()) <= TOL, early
+
+
 def test_split_acc_slab_bf16():
     """The bf16 per-image fp-half slab of the bf16 contract (TMR_SPLIT_OUT_BF16
     on the store, TMR_SPLIT_INIT_BF16 on the heads launch): heads partials from
