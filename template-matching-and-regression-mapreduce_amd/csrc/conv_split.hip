@@ -83,6 +83,9 @@ constexpr int TW = 32;       // output cols per block
 #ifndef TMR_SPLIT_HOIST_HOFF  // halo DMA per-lane offsets computed once (VGPRs) instead of per DMA
 #define TMR_SPLIT_HOIST_HOFF 1
 #endif
+#ifndef TMR_SPLIT_LO3  // F16X3 lo half-chunks in longer steps (see Geo::LO3)
+#define TMR_SPLIT_LO3 1
+#endif
 #ifndef TMR_SPLIT_NW
 #define TMR_SPLIT_NW 8
 #endif
@@ -213,6 +216,23 @@ struct Geo {
     static constexpr int WB = TPS * WB1;                       // bytes per weight buffer
     static constexpr int Q = (MPW + SPC - 1) / SPC;            // halo DMAs per wave issued per step
     static constexpr size_t LDS = 2 * (size_t)HB + NWB * (size_t)WB;
+    // LO3: F16X3 lo half-chunks (one weight term: half a hi tap's bytes) in
+    // steps of up to 2 TPS taps, balanced (3 x 3 at k = 3): fewer barrier
+    // steps per chunk (10 -> 8).  One weight lookahead step (NWB == 2) only.
+    // Measured (r02bm, A/B in one call): fp32 heads 28.02/28.17 -> 27.89/27.97
+    // ms per 48 units, config B 451.3/451.5 -> 454.4/454.1 images/s.
+    static constexpr bool LO3 = TMR_SPLIT_LO3 && PREC == TMR_PREC_F16X3 && NWB == 2 && T > 1;
+    static constexpr int SPCL = LO3 ? (T + 2 * TPS - 1) / (2 * TPS) : SPC;
+    static constexpr int TPSL = LO3 ? (T + SPCL - 1) / SPCL : TPS;
+    static constexpr int SPCC = Prec<PREC>::HALVES == 2 ? SPC + SPCL : SPC;  // steps per chunk
+    static constexpr int tps(int part) { return part ? TPSL : TPS; }
+    static constexpr int spc(int part) { return part ? SPCL : SPC; }
+    static constexpr int wb1(int part) { return (LO3 && part) ? WB1 / 2 : WB1; }
+    static constexpr int qh(int part) { return (MPW + spc(part) - 1) / spc(part); }
+    static constexpr int nhp(int part, int sg) {
+        return MPW - sg * qh(part) < qh(part) ? (MPW - sg * qh(part) > 0 ? MPW - sg * qh(part) : 0) : qh(part);
+    }
+    static constexpr int ntapp(int part, int sg) { return T - sg * tps(part) < tps(part) ? T - sg * tps(part) : tps(part); }
     // per-wave DMA counts of step sg of a half-chunk of kind `part` (the
     // kernel issues, in this order, the step's share of the next halo, then
     // the weights of step g + NWB - 1)
@@ -363,6 +383,17 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     auto w_dma1 = [&](int g, int ipt, int m) {
         buffer_lds16(wr, (lds_ptr_t)w_dst(g, ipt, m), wlane, w_src(g, ipt, m));
     };
+    // LO3: weights of step sgx of half-chunk (cx, px) (the flat step index no
+    // longer determines the shape)
+    auto w_dma3 = [&](int cx, int px, int sgx, int ipt, int m) {
+        const int i = wave + NWAVES * m;
+        const int tl = i / ipt, wi = i - tl * ipt;
+        const uint32_t src = (uint32_t)(sgx * G::tps(px) + tl) * tapstride + (uint32_t)cx * a.Npad * WREC + wnt +
+                             (uint32_t)(wi >> 1) * a.Npad * 16 + (wi & 1) * 64 * 16;
+        const int gbx = cx * G::SPCC + (px ? SPC : 0) + sgx;
+        char *dst = Ws + (gbx % NWB) * WB + tl * G::wb1(px) + wi * 1024;
+        buffer_lds16(wr, (lds_ptr_t)dst, wlane, src);
+    };
 
     // accumulators start at acc_init (scaled into the accumulator's units by
     // the exact power of two s_x s_w); masked elements read a clamped legal
@@ -448,22 +479,35 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
             // waits are constants): step(integral_constant<int, sg>)
             auto step = [&](auto sg_c) {
                 constexpr int sg = decltype(sg_c)::value;
-                const int g = hc * SPC + sg;
+                constexpr bool L3 = G::LO3;
+                constexpr int TPSx = L3 ? G::tps(part) : TPS;
+                const int g = L3 ? c * G::SPCC + (part ? SPC : 0) + sg : hc * SPC + sg;
                 // DMAs for later steps, issued one per pixel-tile MFMA group
                 // from the step's second group on (not in the post-barrier
                 // bubble): first this step's share of the halo of half-chunk
                 // hc+1 (buffer last read in hc-1), then the weights of step
                 // g+D (buffer last read in g-1).  Counts are compile-time and
                 // the same in every wave.
-                constexpr int nh = G::nh(sg);
-                constexpr bool loD = G::lo_of(sg + D, part, HALVES);
-                constexpr int nw = G::nw(sg, part, HALVES);
+                // LO3: the next step is (part, sg+1), the lo half-chunk's step 0
+                // or the next chunk's hi step 0
+                constexpr bool lastx = sg + 1 >= G::spc(part);
+                constexpr int pn = lastx ? 1 - part : part, sgn = lastx ? 0 : sg + 1;
+                constexpr int nh = L3 ? G::nhp(part, sg) : G::nh(sg);
+                constexpr bool loD = L3 ? pn == 1 : G::lo_of(sg + D, part, HALVES);
+                constexpr int nw = L3 ? G::ntapp(pn, sgn) * G::ipt(pn == 1) / NWAVES : G::nw(sg, part, HALVES);
                 constexpr int NSLOT = nh + nw;
                 auto dma_slot = [&](int k) {  // slot k of this step (k < NSLOT)
-                    if (k < nh)
-                        halo_dma1(hc + 1, sg * Q + k);
-                    else
-                        w_dma1(g + D, ipt_of(loD), k - nh);
+                    if constexpr (L3) {
+                        if (k < nh)
+                            halo_dma1(hc + 1, sg * G::qh(part) + k);
+                        else
+                            w_dma3(lastx && part == 1 ? c + 1 : c, pn, sgn, ipt_of(loD), k - nh);
+                    } else {
+                        if (k < nh)
+                            halo_dma1(hc + 1, sg * Q + k);
+                        else
+                            w_dma1(g + D, ipt_of(loD), k - nh);
+                    }
                 };
                 const char *wl = Ws + (g % NWB) * WB;
                 // Register pipeline: the A (weight) fragments of a tap are
@@ -476,9 +520,10 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
                 constexpr int DB = NA >= 8 ? 1 : 2;
                 constexpr int APG = NA >= 8 ? NA / 8 : 1;  // next-tap A reads per pixel tile
                 constexpr int NB = DB + 1;
-                constexpr int ntap = T - sg * TPS < TPS ? T - sg * TPS : TPS;
+                constexpr int ntap = L3 ? G::ntapp(part, sg) : (T - sg * TPS < TPS ? T - sg * TPS : TPS);
+                constexpr int WB1x = L3 ? G::wb1(part) : WB1;
                 auto afrag = [&](int tl, int i) -> V {  // term i / NIN, n fragment i % NIN
-                    return *reinterpret_cast<const V *>(wl + tl * WB1 + (i / NIN) * 4 * WPL + aoff +
+                    return *reinterpret_cast<const V *>(wl + tl * WB1x + (i / NIN) * 4 * WPL + aoff +
                                                         (i % NIN) * 256);
                 };
                 auto bfrag = [&](int tap, int jp) -> V {
@@ -491,12 +536,12 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
                 for (int i = 0; i < NA; ++i) aw[0][i] = afrag(0, i);
 #pragma unroll
-                for (int d = 0; d < DB; ++d) bx[d] = bfrag(sg * TPS, d);
+                for (int d = 0; d < DB; ++d) bx[d] = bfrag(sg * TPSx, d);
                 __builtin_amdgcn_sched_group_barrier(0x100, NA + DB, 0);
 #pragma unroll
-                for (int tl = 0; tl < TPS; ++tl) {
+                for (int tl = 0; tl < TPSx; ++tl) {
                     if (tl >= ntap) break;
-                    const int tap = sg * TPS + tl;
+                    const int tap = sg * TPSx + tl;
                     const bool more = tl + 1 < ntap;
 #pragma unroll
                     for (int jp = 0; jp < 8; ++jp) {
@@ -545,7 +590,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
             };
             [&]<int... SG>(std::integer_sequence<int, SG...>) {
                 (step(std::integral_constant<int, SG>{}), ...);
-            }(std::make_integer_sequence<int, SPC>{});
+            }(std::make_integer_sequence<int, G::LO3 ? G::spc(part) : SPC>{});
         };
         half_chunk(std::integral_constant<int, 0>{});
         if constexpr (HALVES == 2) half_chunk(std::integral_constant<int, 1>{});
