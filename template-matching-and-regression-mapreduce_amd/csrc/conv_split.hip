@@ -83,6 +83,9 @@ constexpr int TW = 32;       // output cols per block
 #ifndef TMR_SPLIT_HOIST_HOFF  // halo DMA per-lane offsets computed once (VGPRs) instead of per DMA
 #define TMR_SPLIT_HOIST_HOFF 1
 #endif
+#ifndef TMR_XPACK4  // activation records 4 pixels per thread (xpack4_kernel)
+#define TMR_XPACK4 1
+#endif
 #ifndef TMR_SPLIT_LO3  // F16X3 lo half-chunks in longer steps (see Geo::LO3)
 #define TMR_SPLIT_LO3 1
 #endif
@@ -861,6 +864,87 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
     }
 }
 
+// MODE 0 with W % 4 == 0: one 256-thread block per (image, chunk, row, 128-px
+// segment) stages the segment's 32 channel rows in LDS from 16-B loads, then
+// every thread forms (pixel, 8-channel piece) records and stores them
+// pixel-contiguous (1 KB per wave store).  Blocks past `nseg` write the
+// padding ring (zero records: the split of 0 is 0 in every term).  Records
+// are bit-identical to xpack_kernel<PREC, 0>'s.
+constexpr int XSEG = 128;
+template <int PREC>
+__global__ __launch_bounds__(256) void xpack4_kernel(const float *__restrict__ x, int S, int Cin, int H, int W,
+                                                     int NCc, int Hp, int Wp, int pad, int64_t nseg,
+                                                     int64_t nbord, const float *__restrict__ xmax,
+                                                     typename Prec<PREC>::V *__restrict__ out) {
+    constexpr int HALVES = Prec<PREC>::HALVES;
+    typedef typename Prec<PREC>::V V;
+    typedef typename Prec<PREC>::E E;
+    __shared__ float tile[CCH][XSEG];
+    const size_t plane = (size_t)Hp * Wp;
+    const int t = threadIdx.x;
+    if ((int64_t)blockIdx.x < nseg) {
+        const int nsx = (W + XSEG - 1) / XSEG;
+        int64_t r = blockIdx.x;
+        const int sx = (int)(r % nsx);
+        r /= nsx;
+        const int y = (int)(r % H);
+        r /= H;
+        const int c = (int)(r % NCc);
+        const int s = (int)(r / NCc);
+        const int x0 = sx * XSEG, nx = min(XSEG, W - x0);  // nx % 4 == 0
+        const float *src = x + ((size_t)s * Cin + (size_t)c * CCH) * H * W + (size_t)y * W + x0;
+#pragma unroll
+        for (int k = 0; k < CCH * XSEG / 4 / 256; ++k) {
+            const int e = t + 256 * k, ch = e / (XSEG / 4), x4 = e % (XSEG / 4);
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (4 * x4 < nx && c * CCH + ch < Cin)
+                v = *reinterpret_cast<const float4 *>(src + (size_t)ch * H * W + 4 * x4);
+            *reinterpret_cast<float4 *>(&tile[ch][4 * x4]) = v;
+        }
+        __syncthreads();
+        const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
+        V *o = out + ((size_t)s * NCc + c) * HALVES * P * plane + (size_t)(y + pad) * Wp + x0 + pad;
+#pragma unroll
+        for (int k = 0; k < XSEG * P / 256; ++k) {
+            const int e = t + 256 * k, q = e / XSEG, px = e % XSEG;
+            if (px < nx) {
+                V hi, lo;
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {  // split_record's arithmetic
+                    const float xs = tile[q * 8 + m][px] * sc;
+                    const E h = (E)xs;
+                    hi[m] = h;
+                    if (HALVES == 2) lo[m] = (E)(xs - (float)h);
+                }
+                o[q * plane + px] = hi;
+                if (HALVES == 2) o[(P + q) * plane + px] = lo;
+            }
+        }
+        return;
+    }
+    // padding ring of plane set (s, c): top rows, bottom rows, then the
+    // left/right columns of the interior rows
+    const int64_t b0 = ((int64_t)blockIdx.x - nseg) * 256 + t;
+    if (b0 >= nbord * S * NCc) return;
+    const int64_t sc_i = b0 / nbord;
+    int64_t b = b0 - sc_i * nbord;
+    const int64_t top = (int64_t)pad * Wp, bot = (int64_t)(Hp - H - pad) * Wp;
+    int yp, xp;
+    if (b < top) {
+        yp = (int)(b / Wp), xp = (int)(b % Wp);
+    } else if ((b -= top) < bot) {
+        yp = H + pad + (int)(b / Wp), xp = (int)(b % Wp);
+    } else {
+        b -= bot;
+        const int side = Wp - W, k = (int)(b % side);
+        yp = pad + (int)(b / side), xp = k < pad ? k : W + k;
+    }
+    V *o = out + (size_t)sc_i * HALVES * P * plane + (size_t)yp * Wp + xp;
+    const V z = {};
+#pragma unroll
+    for (int q = 0; q < HALVES * P; ++q) o[q * plane] = z;
+}
+
 // Fold the decoder's fp half through input_proj (matching_net.py:27-30,56):
 // conv(proj(x)) = conv'([x; 1]) with W'[n][c][t] = sum_k Wd[n][k][t] P[k][c]
 // (c < Cin) and W'[n][Cin][t] = sum_k Wd[n][k][t] b[k]; fp64 accumulation.
@@ -979,6 +1063,25 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
     const dim3 grid((unsigned)tmr_cdiv(total, 256)), blk(256);
     hipStream_t s = tmr_stream(stream);
+    // one-term records from LDS-transposed row segments (bf16 0.61 -> 0.50 ms
+    // per 48 units at 128^2, r02bo3); the 3-term records stay on the
+    // one-pixel kernel (0.61 vs 0.73 ms: twice the stores per staged byte)
+    if (TMR_XPACK4 && MODE == 0 && W % 4 == 0 && prec != TMR_PREC_F16X3) {
+        const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
+        const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
+        switch (prec) {
+            case TMR_PREC_BF16:
+                hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_BF16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
+                                   ks / 2, nseg, nbord, nullptr, static_cast<b8 *>(out));
+                break;
+            default:
+                hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_F16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
+                                   ks / 2, nseg, nbord, xmax, static_cast<h8 *>(out));
+                break;
+        }
+        TMR_CHECK_LAUNCH();
+        return TMR_OK;
+    }
     switch (prec) {
         case TMR_PREC_F16X3:
             hipLaunchKernelGGL((xpack_kernel<TMR_PREC_F16X3, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,

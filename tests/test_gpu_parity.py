@@ -308,6 +308,51 @@ def test_upsample2x_tiled_and_projection_order(Hin, Win):
         assert normwise(fp.cpu().numpy(), ref.numpy()) <= TOL, early
 
 
+def _xrecords_ref(x, ks, prec, xmax):
+    """tmr_split_xpack's record layout restated in torch: [s][chunk][half]
+    [piece q][Hp][Wp][8 x 16-bit], hi = fl16(x s), lo = fl16(x s - hi) (F16X3),
+    s = 2^(14 - e) with max|x| < 2^e (conv_split.hip split_scale), zero ring."""
+    S, C, H, W = x.shape
+    NCc, pad = (C + 31) // 32, ks // 2
+    Hp, Wp = -(-H // 16) * 16 + ks - 1, -(-W // 32) * 32 + ks - 1
+    xs = torch.zeros(S, NCc * 32, Hp, Wp, dtype=torch.float32, device=x.device)
+    sc = 1.0
+    if prec != "bf16":
+        e = int(np.frexp(np.float32(xmax))[1])
+        sc = float(2.0 ** (14 - e))
+    xs[:, :C, pad:pad + H, pad:pad + W] = x * sc
+    dt = torch.bfloat16 if prec == "bf16" else torch.float16
+    hi = xs.to(dt)
+    halves = [hi]
+    if prec == "fp32":
+        halves.append((xs - hi.float()).to(dt))
+    # [S][NCc][32][Hp][Wp] -> [S][NCc][P=4][Hp][Wp][8]
+    recs = [h.view(S, NCc, 4, 8, Hp, Wp).permute(0, 1, 2, 4, 5, 3) for h in halves]
+    return torch.stack(recs, 2).contiguous().view(torch.int16).flatten()
+
+
+@pytest.mark.parametrize("S,C,H,W,ks", [(2, 40, 19, 36, 3), (1, 64, 128, 128, 3), (3, 33, 8, 12, 1),
+                                        (2, 32, 9, 20, 5), (2, 40, 19, 37, 3), (1, 8, 16, 32, 1)])
+def test_xpack_records_bitexact(S, C, H, W, ks):
+    """Activation records (the 4-pixel kernel for W % 4 == 0, the one-pixel
+    kernel otherwise) bit-exact against the torch restatement of the layout,
+    padding ring included (the buffer is pre-filled with garbage)."""
+    from tmr_amd._lib import PREC_CODES, call, load, ptr, stream
+    from tmr_amd.engine import absmax
+    torch.manual_seed(11)
+    x = (torch.randn(S, C, H, W) * 3).cuda()
+    xmax = absmax(x)
+    for prec in ("fp32", "bf16", "f16"):
+        n = load().tmr_split_xpack_size(S, C, H, W, ks, PREC_CODES[prec])
+        out = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
+        call("tmr_split_xpack", ptr(x), S, C, H, W, ks, PREC_CODES[prec], ptr(xmax), ptr(out), stream())
+        ref = _xrecords_ref(x, ks, prec, float(xmax.item()))
+        got = out.view(torch.int16)
+        assert got.numel() == ref.numel(), prec
+        bad = int((got != ref).sum())
+        assert bad == 0, f"{prec}: {bad} of {ref.numel()} 16-bit words differ"
+
+
 def test_split_acc_slab_bf16():
     """The bf16 per-image fp-half slab of the bf16 contract (TMR_SPLIT_OUT_BF16
     on the store, TMR_SPLIT_INIT_BF16 on the heads launch): heads partials from
