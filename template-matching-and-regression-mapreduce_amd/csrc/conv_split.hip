@@ -870,7 +870,13 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
 // pixel-contiguous (1 KB per wave store).  Blocks past `nseg` write the
 // padding ring (zero records: the split of 0 is 0 in every term).  Records
 // are bit-identical to xpack_kernel<PREC, 0>'s.
-constexpr int XSEG = 128;
+#ifndef TMR_XSEG
+#define TMR_XSEG 128
+#endif
+#ifndef TMR_XPACK4_3T  // 3-term records on xpack4_kernel too (measured slower, r02bo3)
+#define TMR_XPACK4_3T 0
+#endif
+constexpr int XSEG = TMR_XSEG;
 template <int PREC>
 __global__ __launch_bounds__(256) void xpack4_kernel(const float *__restrict__ x, int S, int Cin, int H, int W,
                                                      int NCc, int Hp, int Wp, int pad, int64_t nseg,
@@ -1066,10 +1072,16 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
     // one-term records from LDS-transposed row segments (bf16 0.61 -> 0.50 ms
     // per 48 units at 128^2, r02bo3); the 3-term records stay on the
     // one-pixel kernel (0.61 vs 0.73 ms: twice the stores per staged byte)
-    if (TMR_XPACK4 && MODE == 0 && W % 4 == 0 && prec != TMR_PREC_F16X3) {
+    if (TMR_XPACK4 && MODE == 0 && W % 4 == 0 && (TMR_XPACK4_3T || prec != TMR_PREC_F16X3)) {
         const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
         const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
         switch (prec) {
+#if TMR_XPACK4_3T
+            case TMR_PREC_F16X3:
+                hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_F16X3>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
+                                   ks / 2, nseg, nbord, xmax, static_cast<h8 *>(out));
+                break;
+#endif
             case TMR_PREC_BF16:
                 hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_BF16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
                                    ks / 2, nseg, nbord, nullptr, static_cast<b8 *>(out));
