@@ -12,6 +12,13 @@ per-image counts and kept boxes that replaces the Hadoop reducer).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+`python bench.py --gpus N` (N > 1) outside a torch.distributed launch starts
+the N rank processes itself (torch.distributed.run, 127.0.0.1, one per GPU)
+before anything touches the GPU, and exits with their status; launched by
+torchrun, WORLD_SIZE must equal --gpus.  The reference's counterparts are
+Lightning DDP over all devices (main.py:108-119) and Hadoop's map-side
+parallelism (mapper.py:51).
+
 Prints one JSON line (rank 0).  `roofline` is the fused decoder kernel
 (tmr_conv_heads, >98% of the path's FLOPs) timed with HIP events on its
 launch stream; `cpu_baseline` is the CPU oracle (torch-CPU restatement of the
@@ -22,14 +29,48 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 REPO = os.path.dirname(os.path.abspath(__file__))
+
+
+def launch_plan(argv, env):
+    """What `bench.py argv` must do about ranks, decided before torch or the
+    package is imported: None = run here as this rank; a command list = start
+    the N rank processes with it and exit with their status.  Raises
+    SystemExit(2) when a torch.distributed launch disagrees with --gpus."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args(argv)[0].gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != n:
+            print(f"bench.py: refusing to run: WORLD_SIZE={world} but --gpus {n}", file=sys.stderr)
+            raise SystemExit(2)
+        return None
+    if n == 1:
+        return None
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:  # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+if __name__ == "__main__":
+    _cmd = launch_plan(sys.argv[1:], os.environ)
+    if _cmd is not None:  # this process never touches the GPU: the ranks are children
+        sys.exit(subprocess.call(_cmd))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, REPO)
 from tmr_import import load_package  # noqa: E402
 
@@ -70,14 +111,42 @@ def decoder_flops_per_unit() -> float:
     return 2.0 * H * W * (2 * 2 * EMB) * (2 * EMB * KS * KS)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores() -> int:
+    """The cores this process may run on: its CPU affinity, capped by a
+    cgroup-v2 CPU quota (a GPU box's share of a larger host: os.cpu_count()
+    counts the whole machine there, and more threads than the quota would
+    only time-slice)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(P, feats, ex, seconds: float, cls: float, iou: float):
     """The reference forward on the host cores: torch-CPU restatement
     (oracle/oracle.py, op for op the reference's ATen calls, one full forward
-    per exemplar like demo.py:111) + C peaks/NMS.  Bounded by `seconds`."""
+    per exemplar like demo.py:111) + C peaks/NMS.  Bounded by `seconds`.
+    Threads: every core available to the process."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     Pc = {k: v.detach().cpu() for k, v in P.items()}
     t0 = time.perf_counter()
@@ -98,8 +167,11 @@ def cpu_baseline(P, feats, ex, seconds: float, cls: float, iou: float):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{n} image(s) x {ex.shape[1]} exemplars of the same workload, "
-                      f"{dt:.1f} s, torch {torch.__version__} CPU ({threads} threads)"}
+                      f"{dt:.1f} s, torch {torch.__version__} CPU ({threads} threads = the cores "
+                      f"available to the process; the host reports {os.cpu_count()} CPUs, "
+                      f"{cpu_model()})"}
 
 
 def xcorr_by_class(eng, feats_d, ex, reps: int = 3):
@@ -134,18 +206,21 @@ def xcorr_by_class(eng, feats_d, ex, reps: int = 3):
     return out
 
 
-def load_traffic(algo: str, prec: str):
-    """Per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE, raw) of the decoder
-    kernel from the committed rocprofv3 PMC summary of the current kernel
-    version (profiles/decoder_pmc.json, keyed by kernel variant), or None."""
-    p = os.path.join(REPO, "profiles", "decoder_pmc.json")
-    if os.path.exists(p):
-        with open(p) as fh:
-            d = json.load(fh)
-        rec = d.get(f"{algo}_{prec}") if isinstance(d.get(f"{algo}_{prec}"), dict) else None
-        if rec is not None:
-            return rec.get("hbm_bytes_per_launch")
-    return None
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_by_config.json")
+
+
+def load_pmc(config: str, role: str):
+    """The committed rocprofv3 PMC record (profiles/pmc_by_config.json,
+    assembled by profiles/pmc_assemble.py) of this config's `role` kernel
+    launch ("heads", "store", "xcorr"), or None when none was collected."""
+    if not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as fh:
+        d = json.load(fh)
+    rec = d.get("configs", {}).get(config, {}).get(role)
+    if isinstance(rec, dict):
+        rec = dict(rec, source=f"profiles/pmc_by_config.json round {d.get('round')}")
+    return rec
 
 
 def main():
@@ -164,7 +239,13 @@ def main():
                          "the reference's per-exemplar module calls (demo.py:106-130)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-xcorr-classes", action="store_true",
+                    help="skip the per-template-class correlation launches after the timed region "
+                         "(PMC passes: one launch per kernel role)")
     a = ap.parse_args()
+    # the committed PMC records describe each config's own workload only
+    own_options = (a.batch is None and a.exemplars is None and a.precision is None
+                   and a.decoder == "split" and a.path == "detect")
 
     rank, world, local = driver.dist_env()
     # one process per GPU; a rehearsal with more ranks than GPUs (gloo on a
@@ -296,7 +377,22 @@ def main():
         if eng.last_shared_flops == 0.0:
             alg_flops *= 2
         alg_achieved = alg_flops / avg_s / 1e12
-        path_alg = decoder_flops_per_unit() * B * E  # both decoders, whole path per step
+        # whole path, EXECUTED MFMA-class work per step (SURVEY.md §7.3.2 / §8d:
+        # when the fp half is shared across an image's exemplars, the fraction
+        # is taken against the work actually executed): the decoders' f_TM
+        # half per unit, their fp half (folded through input_proj, K = 256*9)
+        # once per image when shared (else per unit), and the 1x1 projection
+        # at the SAM features' size once per image; counted at one term
+        shared = (eng.last_shared_flops > 0.0) if a.path == "detect" else E > 1
+        S = H * W
+        dec_tm = 2.0 * S * (4 * EMB) * (EMB * KS * KS) * B * E
+        dec_fp = 2.0 * S * (4 * EMB) * (CIN * KS * KS) * (B if shared else B * E)
+        proj = 2.0 * CIN * EMB * (S // 4) * B
+        path_exec = dec_tm + dec_fp + proj
+        path_ref = decoder_flops_per_unit() * B * E  # the reference's count: both halves per unit
+        xc_flops, xc_bytes, xc_dram = eng.last_xcorr_flops, eng.last_xcorr_bytes, eng.last_xcorr_dram_bytes
+        pmc_heads = load_pmc(a.config, "heads") if own_options else None
+        pmc_xc = load_pmc(a.config, "xcorr") if own_options else None
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
@@ -311,17 +407,31 @@ def main():
             "roofline": {"bound": "mfma", "kernel": kernel_name,
                          "achieved": round(alg_achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(alg_achieved / peak, 4),
-                         "traffic": load_traffic(algo, prec), "avg_launch_ms": round(1e3 * avg_s, 3),
+                         "traffic": pmc_heads.get("hbm_bytes_per_launch") if pmc_heads else None,
+                         "traffic_source": (pmc_heads["source"] + " (FETCH_SIZE x2 + WRITE_SIZE of this "
+                                            "config's heads launch; its kernel-trace average %.3f ms)"
+                                            % (1e3 * pmc_heads.get("avg_launch_s", float("nan"))))
+                         if pmc_heads else "no PMC record for this config/options",
+                         "mfma_busy_pmc": round(pmc_heads["mfma_busy_frac"], 4)
+                         if pmc_heads and "mfma_busy_frac" in pmc_heads else None,
+                         "avg_launch_ms": round(1e3 * avg_s, 3),
                          "flops_per_launch": alg_flops,
                          "flops_basis": "algorithmic (SURVEY.md 8d): 2*H*W*N(2048)*K(512*9) per unit, the "
                                         "decoder_b+decoder_o conv over the f_TM half (x2 when E=1: both "
-                                         "halves in this launch); peak = dense 16-bit MFMA",
+                                        "halves in this launch); peak = dense 16-bit MFMA",
                          "executed_achieved": round(executed_achieved, 2),
                          "executed_frac": round(executed_achieved / peak, 4),
                          "executed_basis": flops_basis,
-                         "path_algorithmic_tflop_per_step": round(path_alg / 1e12, 2),
-                         "path_achieved": round(path_alg / (ms_step / 1e3) / 1e12, 2),
-                         "path_frac": round(path_alg / (ms_step / 1e3) / 1e12 / peak, 4)},
+                         "path_executed_tflop_per_step": round(path_exec / 1e12, 3),
+                         "path_achieved": round(path_exec / (ms_step / 1e3) / 1e12, 2),
+                         "path_frac": round(path_exec / (ms_step / 1e3) / 1e12 / peak, 4),
+                         "path_basis": ("executed work per step at one term per product: decoders' f_TM "
+                                        "half per unit + fp half (folded, K=256*9) %s + 1x1 projection "
+                                        "per image, / step time / dense 16-bit MFMA peak"
+                                        % ("once per image (shared by its exemplars)" if shared
+                                           else "per unit")),
+                         "path_reference_tflop_per_step": round(path_ref / 1e12, 2),
+                         "path_reference_equiv_frac": round(path_ref / (ms_step / 1e3) / 1e12 / peak, 4)},
         }
         # the correlation kernel (SURVEY.md 8d "kernel 2"): HBM-bound for small
         # templates, VALU-bound for k >= 11; both fractions, algorithmic work
@@ -339,13 +449,21 @@ def main():
             "algo": xk,
             "bound": "hbm" if cfg["kmax"] <= 9 else "valu",
             "avg_launch_ms": round(1e3 * xs, 3),
-            "hbm_achieved": round(eng.last_xcorr_bytes / xs / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
-            "hbm_unit": "GB/s", "hbm_frac": round(eng.last_xcorr_bytes / xs / 1e9 / HBM_PEAK_GBS, 4),
-            "valu_achieved": round(eng.last_xcorr_flops / xs / 1e12, 2), "valu_peak": FP32_PEAK_TFLOPS,
-            "valu_unit": "TFLOP/s", "valu_frac": round(eng.last_xcorr_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "basis": "per unit: read + write C*H*W fp32 (the fp plane read once per unit, f_TM written), "
-                     "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)",
-            "by_class": xcorr_by_class(eng, feats_d, ex)}
+            "hbm_achieved": round(xc_bytes / xs / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
+            "hbm_unit": "GB/s", "hbm_frac": round(xc_bytes / xs / 1e9 / HBM_PEAK_GBS, 4),
+            "dram_min_bytes_per_launch": xc_dram,
+            "dram_min_achieved": round(xc_dram / xs / 1e9, 1),
+            "dram_min_frac": round(xc_dram / xs / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": pmc_xc.get("hbm_bytes_per_launch") if pmc_xc else None,
+            "traffic_source": pmc_xc["source"] if pmc_xc else "no PMC record for this config/options",
+            "valu_achieved": round(xc_flops / xs / 1e12, 2), "valu_peak": FP32_PEAK_TFLOPS,
+            "valu_unit": "TFLOP/s", "valu_frac": round(xc_flops / xs / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "basis": "hbm_*: SURVEY.md 8d bytes, read + write C*H*W fp32 per unit (the fp plane counted "
+                     "once per unit); dram_min_*: the bytes the launch must move (each image's fp plane "
+                     "read once for all its units, one f_TM plane written per unit); "
+                     "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)"}
+        if not a.no_xcorr_classes:
+            out["roofline_xcorr"]["by_class"] = xcorr_by_class(eng, feats_d, ex)
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds, cfg["cls"], cfg["iou"])
         else:

@@ -1,7 +1,8 @@
 """Per-launch averages of rocprofv3 --pmc counters (CSV output, one counter
-set per pass/run) for the kernels whose name contains a substring.
+set per pass/run) for the kernels whose name matches a regular expression
+(a plain substring works as one).
 
-    python profiles/pmc_csv.py <kernel-substring> <dir-or-csv>...
+    python profiles/pmc_csv.py <kernel-regex> <dir-or-csv>...
 
 Prints {counter: mean per launch} plus launch counts as JSON.  HBM byte
 conventions (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE are in KB;
@@ -14,6 +15,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -22,12 +24,13 @@ def collect(kernel, paths):
     largest grid (a kernel's small side launches, e.g. the one-off bias-plane
     launch of split_conv_kernel<3,0,0>, are left out of the averages)."""
     rows = []
+    pat = re.compile(kernel)
     for p in paths:
         files = glob.glob(os.path.join(p, "**", "*counter_collection.csv"), recursive=True) \
             if os.path.isdir(p) else [p]
         for f in files:
             for row in csv.DictReader(open(f)):
-                if kernel in row["Kernel_Name"]:
+                if pat.search(row["Kernel_Name"]):
                     rows.append((f, row))
     gmax = max((int(r["Grid_Size"]) for _, r in rows), default=0)
     vals = collections.defaultdict(list)

@@ -319,6 +319,7 @@ class TMREngine:
         self.xcorr_events = None
         self.last_xcorr_flops = 0.0
         self.last_xcorr_bytes = 0.0
+        self.last_xcorr_dram_bytes = 0.0
         # conv(cat[fp, f_TM]) = conv_fp(fp) + conv_tm(f_TM): compute conv_fp once
         # per image when several exemplars share it (fp32, changes only the
         # summation order; same 1e-5 contract)
@@ -609,6 +610,10 @@ class TMREngine:
         ht, wt = units["ht"].astype(np.float64), units["wt"].astype(np.float64)
         self.last_xcorr_flops = float(np.sum(2.0 * C * (H - ht + 1) * (W - wt + 1) * ht * wt))
         self.last_xcorr_bytes = 2.0 * 4 * C * H * W * U
+        # the minimum DRAM traffic of this launch: the kernels stage each
+        # image's fp plane once for all its units (read once per IMAGE), and
+        # write one f_TM plane per unit
+        self.last_xcorr_dram_bytes = 4.0 * C * H * W * (len(set(int(i) for i in unit_image)) + U)
         self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 

@@ -1,0 +1,74 @@
+"""bench.py's rank launcher (CPU): `python bench.py --gpus N` outside a
+torch.distributed launch must start N rank processes (one per GPU, the
+reference's Lightning DDP over all devices, main.py:108-119) before anything
+touches the GPU; under torchrun, WORLD_SIZE must equal --gpus."""
+import importlib.util
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_single_gpu_runs_in_process():
+    b = _bench()
+    assert b.launch_plan([], {}) is None
+    assert b.launch_plan(["--gpus", "1", "--steps", "2"], {}) is None
+
+
+def test_multi_gpu_spawns_ranks():
+    b = _bench()
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "2"]
+    cmd = b.launch_plan(argv, {})
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert any(c.startswith("--master-port=") and int(c.split("=")[1]) > 0 for c in cmd)
+    assert cmd[-len(argv) - 1] == os.path.join(REPO, "bench.py")
+    assert cmd[-len(argv):] == argv  # the ranks see the same --gpus and see WORLD_SIZE
+
+
+def test_ranks_under_torchrun_run_in_process():
+    b = _bench()
+    assert b.launch_plan(["--gpus", "4"], {"WORLD_SIZE": "4"}) is None
+
+
+def test_world_size_mismatch_refused():
+    b = _bench()
+    with pytest.raises(SystemExit) as e:
+        b.launch_plan(["--gpus", "8"], {"WORLD_SIZE": "2"})
+    assert e.value.code == 2
+    # end to end: refused before torch or the package is imported
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "refusing" in r.stderr
+
+
+def test_launcher_starts_children_and_returns_their_status(tmp_path):
+    """The launch path never imports torch in the parent: a fake
+    torch.distributed.run on PYTHONPATH records its argv and exits 3; bench.py
+    must exit with that status."""
+    pkg = tmp_path / "torch" / "distributed"
+    pkg.mkdir(parents=True)
+    (tmp_path / "torch" / "__init__.py").write_text("")
+    (pkg / "__init__.py").write_text("")
+    rec = tmp_path / "argv.txt"
+    (pkg / "run.py").write_text(f"import sys\nopen({str(rec)!r}, 'w').write(' '.join(sys.argv[1:]))\n"
+                                "sys.exit(3)\n")
+    env = dict(os.environ, PYTHONPATH=str(tmp_path))
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3, r.stderr
+    got = rec.read_text()
+    assert "--nproc-per-node=2" in got and got.endswith("--gpus 2 --steps 1")

@@ -58,19 +58,22 @@ def _oracle_detect_on_maps(prob, reg, boxes, thr, iou):
     return L[0], B[0], R[0]
 
 
-def _check_images(P, feats, ex, images, thr, iou, hf):
+def _check_images(P, feats, ex, images, thr, iou, hf, precision="fp32", tol=TOL):
     """bench-batch run through TMREngine.detect + forward_units; per checked
-    image: maps vs the oracle forward, detect() vs the oracle's peaks+NMS on
-    the GPU's maps (bit-exact), agreement with the oracle's own maps."""
+    image: maps vs the oracle forward (normwise <= tol), detect() vs the
+    oracle's peaks+NMS on the GPU's maps (bit-exact), agreement with the
+    oracle's own maps (held to its contract on the fp32 path; reported only
+    under a reduced-precision contract)."""
     B, E = ex.shape[:2]
     Pd = {k: v.to(DEV) for k, v in P.items()}
-    eng = tmr_amd.TMREngine(Pd, tmr_amd.PathConfig())
+    eng = tmr_amd.TMREngine(Pd, tmr_amd.PathConfig(precision=precision))
     fd = cuda(feats)
     L, Bx, R = eng.detect(fd, ex, cls_ths=thr, iou_threshold=iou)  # the bench step
     ui = np.repeat(np.arange(B), E)
     r = eng.forward_units(fd, ui, ex.reshape(-1, 4))
     o, b = r["o"].cpu().numpy(), r["b"].cpu().numpy()
     lines = []
+    worst = 0.0
     for img in images:
         units = [img * E + e for e in range(E)]
         omaps = []
@@ -78,8 +81,10 @@ def _check_images(P, feats, ex, images, thr, iou, hf):
             ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[img:img + 1]),
                                                 [torch.from_numpy(ex[img, e:e + 1])], P)
             ro, rb = ro[0][0].numpy(), rb[0][0].numpy()
-            assert normwise(o[u], ro) <= TOL, (img, e, normwise(o[u], ro))
-            assert normwise(b[u], rb) <= TOL, (img, e, normwise(b[u], rb))
+            eo, eb = normwise(o[u], ro), normwise(b[u], rb)
+            worst = max(worst, eo, eb)
+            assert eo <= tol, (img, e, eo)
+            assert eb <= tol, (img, e, eb)
             omaps.append((oracle.sigmoid_cr(ro[0]), rb))
         gmaps = agreement.unit_maps(o[units], b[units])
         gl, gb, gr = _oracle_detect_on_maps([m[0] for m in gmaps], [m[1] for m in gmaps],
@@ -88,9 +93,11 @@ def _check_images(P, feats, ex, images, thr, iou, hf):
         assert bits_equal(Bx[img].cpu().numpy(), gb), img
         assert bits_equal(R[img].cpu().numpy(), gr), img
         rep = agreement.compare(omaps, gmaps, list(ex[img]), thr, iou)
-        agreement.check(rep)
-        lines.append(agreement.report_line(f"image {img} oracle-maps vs GPU-maps:", rep))
+        if precision == "fp32":
+            agreement.check(rep)
+        lines.append(agreement.report_line(f"image {img} oracle-maps vs GPU-maps ({precision}):", rep))
     print("\n".join(lines))
+    print(f"{precision} worst normwise map error over the checked units: {worst:.2e} (contract {tol:g})")
     return [int(x.shape[0]) for x in L]
 
 
@@ -101,6 +108,29 @@ def test_headline_batch_config_b():
     ex, _ = synth.exemplar_set(2000, 64, 3, 128, 128, 3, 15)
     kept = _check_images(P, feats, ex, (0, 31, 63), 0.1, 0.5, 64)
     print("config B mean kept per image:", float(np.mean(kept)))
+
+
+def test_headline_batch_config_c():
+    """bench.py config C exactly (seeds 1000 / 2000, 64 x 3, bf16 decoders +
+    one-term bf16 MFMA correlation, bf16 acc0 slabs, one-term record packs at
+    image offsets up to 63, cls 0.25): images 0, 31, 63 within the bf16
+    contract 1e-2 normwise of the fp32 oracle; peaks + NMS bit-exact on the
+    GPU's own maps; agreement with the oracle's maps reported."""
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, 64, 256, 64, 64)
+    ex, _ = synth.exemplar_set(2000, 64, 3, 128, 128, 3, 15)
+    kept = _check_images(P, feats, ex, (0, 31, 63), 0.25, 0.5, 64, precision="bf16", tol=1e-2)
+    print("config C mean kept per image:", float(np.mean(kept)))
+
+
+def test_headline_batch_config_d():
+    """bench.py config D exactly (seeds 1000 / 2000, 64 x 1: the unshared
+    folded fp-half path, cls 0.4): images 0 and 63 within 1e-5."""
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, 64, 256, 64, 64)
+    ex, _ = synth.exemplar_set(2000, 64, 1, 128, 128, 3, 15)
+    kept = _check_images(P, feats, ex, (0, 63), 0.4, 0.5, 64)
+    print("config D mean kept per image:", float(np.mean(kept)))
 
 
 def test_config_e_last_image():

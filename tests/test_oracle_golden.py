@@ -185,3 +185,41 @@ def test_reference_exp_characterised():
     assert (ref != cr).any()
     if exp_table.recorded_cpu(raw) == exp_table.host_cpu():
         assert np.array_equal(ref.view(np.uint32), t.view(np.uint32))
+
+
+def test_reference_exp_table_pinned(tmp_path, monkeypatch):
+    """The reference-exp table is the golden host's: its SHA-256 is pinned,
+    this host's torch.exp matches the committed golden sample, a different
+    table is refused by read(), and generation refuses a host whose torch.exp
+    differs from the golden host's (VERDICT r2 #4)."""
+    from tmr_amd import exp_table
+    from tmr_amd._lib import TMRError
+    assert exp_table.sha256() == exp_table.GOLDEN_SHA256
+    raw = exp_table.read()
+    assert exp_table.recorded_cpu(raw) == exp_table.GOLDEN_CPU
+    ok, bad, n = exp_table.host_matches_golden()
+    if exp_table.host_cpu() == exp_table.GOLDEN_CPU:
+        assert ok, (bad, n)
+    # the sample's recorded half really exercises the table
+    with np.load(exp_table.SAMPLE, allow_pickle=False) as z:
+        x, y = z["x"], z["y"]
+    hit = exp_table.lookup_host(x.view(np.float32), raw)
+    assert 8000 <= int(hit.sum()) <= 8192 + 200
+    cr = np.exp(x.view(np.float32).astype(np.float64)).astype(np.float32).view(np.uint32)
+    assert np.array_equal(hit, y != cr)  # recorded <=> the golden exp is not correctly rounded
+    # a corrupted copy is refused
+    bad_copy = tmp_path / "exp_ref.bin"
+    b = bytearray(open(exp_table.PATH, "rb").read())
+    b[HEADER_FLIP] ^= 1
+    bad_copy.write_bytes(bytes(b))
+    with pytest.raises(TMRError, match="sha256"):
+        exp_table.read(str(bad_copy))
+    # another host's exp: generation refuses before writing anything
+    monkeypatch.setattr(exp_table, "host_matches_golden", lambda sample=None: (False, 17, 16384))
+    out = tmp_path / "gen.bin"
+    with pytest.raises(TMRError, match="differs from the golden host"):
+        exp_table.generate(str(out))
+    assert not out.exists()
+
+
+HEADER_FLIP = 128 + 4 * 40000  # a byte inside the offsets block

@@ -352,15 +352,54 @@ def test_tar_images_and_preprocess(tmp_path):
                             input_shape=(64, 48))
     assert src.counts == n_ok
     for i in range(len(src.items)):
-        path, member, _ = src.items[i]
+        path, member, _, plain = src.items[i]
+        assert plain
         x = src._read(i)
         assert x.shape == (1, 3, 48, 64) and x.dtype == np.float32
         import tarfile
         with tarfile.open(path) as tf:
-            img = Image.open(tf.extractfile(member)).convert("RGB")
+            img = Image.open(tf.extractfile(member.name)).convert("RGB")
         ref = np.asarray(img.resize((64, 48), Image.Resampling.BICUBIC)).astype(np.float32) / np.float32(255.0)
         np.testing.assert_array_equal(x[0], ref.transpose(2, 0, 1))
     assert mr.preprocess_image(b"garbage") is None
+
+
+def test_tar_reads_do_not_rescan_headers(tmp_path, monkeypatch):
+    """an image read must not re-read the shard's headers (a
+    lookup by name walks them all: O(n^2) per shard).  After listing, reading
+    every image of a plain shard opens no TarFile; a gzip shard (no direct
+    offsets) is read through one TarFile per thread, by TarInfo, with the
+    same bytes."""
+    import gzip
+    import shutil
+    import tarfile
+    shards = ["Easy_0.tar", "Hard_1.tar"]
+    _tar_tree(str(tmp_path), shards)
+    src = mr.TarImageSource(str(tmp_path), shards, _PoolBackbone(), torch.device("cpu"), 2, 3, 5, 0,
+                            input_shape=(32, 32))
+    opened = []
+    real_open = tarfile.open
+    monkeypatch.setattr(tarfile, "open", lambda *a, **k: opened.append(a) or real_open(*a, **k))
+    plain_bytes = [mr.read_member(p, m, pl) for p, m, _, pl in src.items]
+    for i in range(len(src.items)):
+        src._read(i)
+    assert opened == []
+    # the same shard gzip-compressed
+    gz = tmp_path / "gz"
+    gz.mkdir()
+    with open(tmp_path / "Easy_0.tar", "rb") as fi, gzip.open(gz / "Easy_0.tar", "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    plain, members = mr.tar_members(str(gz / "Easy_0.tar"))
+    assert not plain
+    import threading
+    tls = threading.local()
+    opened.clear()
+    got = [mr.read_member(str(gz / "Easy_0.tar"), m, plain, tls) for m in members]
+    assert len(opened) == 1
+    want = [b for (p, _, _, _), b in zip(src.items, plain_bytes) if p.endswith("Easy_0.tar")]
+    decodable = {m.name for p, m, _, _ in src.items if p.endswith("Easy_0.tar")}
+    assert [g for g, m in zip(got, members) if m.name in decodable] == want
+    tls.tf.close()
 
 
 def test_tar_source_feature_cache_roundtrip(tmp_path):
