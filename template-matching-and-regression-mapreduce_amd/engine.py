@@ -794,9 +794,14 @@ class TMREngine:
         unit_boxes[u]).  Returns dict(o, b, f_tm_relu, f0, fp)."""
         unit_image = [int(i) for i in unit_image]
         m = self._fp_memo
-        pkey = tuple(self.P[k]._version for k in ("input_proj.0.weight", "input_proj.0.bias"))
+        # the projection memo follows the input_proj parameters' storage,
+        # version AND identity (as _PackCache), and the path options that
+        # change the projection's arithmetic (ADVICE r2)
+        params = (self.P["input_proj.0.weight"], self.P["input_proj.0.bias"])
+        pkey = (_version_key(params), self.cfg.precision, self.proj_before_upsample,
+                self.cfg.feature_upsample)
         if self.reuse_image_work and self._same_image(m, feats) and m[3] == pkey and \
-                self.decoder_algo == "split":
+                all(r() is t for r, t in zip(m[5], params)) and self.decoder_algo == "split":
             fp, f0 = m[4], None
             if want_aux:  # f[0]: a fresh tensor per call, like the reference's
                 f0 = feats
@@ -808,7 +813,8 @@ class TMREngine:
         else:
             fp, f0 = self.project(feats, want_f0=want_aux)
             if self.reuse_image_work:
-                self._fp_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), pkey, fp)
+                self._fp_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), pkey, fp,
+                                 tuple(weakref.ref(t) for t in params))
         if self.cfg.no_matcher:
             ui = _h2d(np.asarray(unit_image, np.int64), fp.device)
             f_tm = fp.index_select(0, ui).contiguous()

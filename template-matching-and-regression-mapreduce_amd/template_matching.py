@@ -74,9 +74,13 @@ class TemplateMatching(nn.Module):
         if h % 2 == 0 or w % 2 == 0:
             raise TMRError("cross_correlation: odd template sizes only (extract_template makes "
                            "them odd, template_matching.py:72-73)")
-        if self.squeeze and bs != 1:
-            raise TMRError("cross_correlation: squeeze sums over bs*c channels; bs must be 1")
         one = torch.ones(1, device=feature.device, dtype=torch.float32)
+        if self.squeeze and bs != 1:
+            # the reference sums the [1, bs*c, H, W] map over all its channels
+            # (:29-35); the per-(b, c) maps come from the kernel, the channel
+            # sum is the reference's own torch.sum
+            f = _xcorr(feature, template, one, False).reshape(1, bs * c, *feature.shape[-2:])
+            return torch.sum(f, dim=1, keepdim=True)
         return _xcorr(feature, template, one, self.squeeze).reshape(
             1, 1 if self.squeeze else bs * c, *feature.shape[-2:])
 

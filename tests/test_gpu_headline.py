@@ -200,6 +200,22 @@ def test_template_matching_module_api():
     assert bits_equal(m.matcher(fd, exl).cpu().numpy(), f)
 
 
+def test_cross_correlation_squeeze_batch():
+    """template_matching.py:23-41 with squeeze and bs > 1: the [1, bs*c, H, W]
+    correlation summed over ALL bs*c channels -> [1, 1, H, W]."""
+    C, H, W = 16, 40, 48
+    f = synth.normal(41, (3, C, H, W))
+    t = synth.normal(42, (3, C, 5, 7))
+    m = tmr_amd.TemplateMatching("roi_align", squeeze=True).to(DEV)
+    got = m.cross_correlation(cuda(f), cuda(t)).cpu().numpy()
+    assert got.shape == (1, 1, H, W)
+    ref = sum(oracle.xcorr(f[b], t[b], 1.0).astype(np.float64).sum(0) for b in range(3))
+    assert normwise(got[0, 0], ref) <= TOL
+    # bs == 1 keeps the kernel's own channel sum
+    m1 = m.cross_correlation(cuda(f[:1]), cuda(t[:1])).cpu().numpy()
+    assert normwise(m1[0, 0], oracle.xcorr(f[0], t[0], 1.0).astype(np.float64).sum(0)) <= TOL
+
+
 def _model_and_inputs(seed=11, B=1, E=3, hf=32, cin=64, emb=64, bias=-0.5):
     args = SimpleNamespace(emb_dim=emb, fusion=True, ablation_no_box_regression=False,
                            encoder="original", feature_upsample=True, no_matcher=False,
@@ -315,6 +331,10 @@ def test_module_reuse_follows_inputs_and_weights():
     with torch.no_grad():
         model.input_proj[0].weight.mul_(1.03)
     check(feats, "input_proj updated")
+    # a NEW Parameter object (version 0 again) between calls on the same features
+    model.input_proj[0].weight = torch.nn.Parameter(model.input_proj[0].weight.detach() * 0.9)
+    model.input_proj[0].bias = torch.nn.Parameter(model.input_proj[0].bias.detach() + 0.01)
+    check(feats, "input_proj replaced")
     with torch.no_grad():
         model.decoder_o.layer[0].weight.mul_(0.97)
     check(feats, "decoder updated")
