@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/tmr.h"
 
@@ -19,6 +20,12 @@
 static inline hipStream_t tmr_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int64_t tmr_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// host-side A/B switch of a measured variant (documented where it is read)
+static inline int tmr_env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
 
 // Near-correctly-rounded fp32 exp / sigmoid: double evaluation, one rounding.
 // The reference's torch.exp / torch.sigmoid bits depend on the backend and on

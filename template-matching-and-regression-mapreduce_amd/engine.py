@@ -19,6 +19,8 @@ MFMA layouts are derived caches, rebuilt when a parameter changes.
 """
 from __future__ import annotations
 
+import json
+import os
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -91,6 +93,41 @@ XCORR_COST = {
         np.interp(XCORR_COST_K, _K192, np.asarray(_T192[a]) / 128.0 / 2.25))
     for a in ("valu", "mfma", "mfma1")
 }
+XCORR_COST_SOURCE = "engine.py tables (HIP events, profiles/r02w_*, r02af_*)"
+# The committed rocprofv3 sweep (profiles/gpu_xcorr_sweep.sh ->
+# profiles/xcorr_sweep_assemble.py -> xcorr_cost.json: kernel-trace launch
+# durations of both kernels per k and regime, recorded beside their FETCH /
+# WRITE bytes and MFMA-busy counters in profiles/xcorr_crossover.json)
+# replaces the tables above when present.
+_COST_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "xcorr_cost.json")
+
+
+def _load_xcorr_cost(path: str = _COST_JSON):
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    reg = d.get("regimes", {})
+
+    def per_unit(name, algo, area):
+        r = reg[name]
+        ks, ms = zip(*sorted((int(k), float(v)) for k, v in r["ms"][algo] if v is not None))
+        return np.interp(XCORR_COST_K, ks, np.asarray(ms) / (r["images"] * r["E"]) / area)
+
+    try:
+        table = {
+            "valu": (per_unit("r128_e3_fp32", "valu", 1.0), per_unit("r192_e16_fp32", "valu", 2.25)),
+            "mfma": (per_unit("r128_e3_fp32", "mfma", 1.0), per_unit("r192_e16_fp32", "mfma", 2.25)),
+            "mfma1": (per_unit("r128_e3_bf16", "mfma", 1.0), per_unit("r192_e16_bf16", "mfma", 2.25)),
+        }
+    except (KeyError, ValueError):
+        return None
+    return table, d.get("source", path)
+
+
+_swept = _load_xcorr_cost()
+if _swept is not None:
+    XCORR_COST, XCORR_COST_SOURCE = _swept
 # A mixed-size MFMA launch stages every band with the LARGEST template's halo
 # rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
 # units when an image has few of them: measured 1.13x the per-k sum at the
