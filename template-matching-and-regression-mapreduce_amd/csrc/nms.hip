@@ -43,6 +43,7 @@ struct NmsWork {
     float *r;        // [T][2]
     int32_t *idx;    // [T] local row index (sort values in)
     int32_t *order;  // [T] sorted position -> local index
+    float *sb;       // [T][4] boxes in sorted order (the strips' row and column operands)
     uint64_t *removed;  // [sum_nb] running suppression bitmap per image
     uint64_t *strip;    // [strip_words]
     char *temp;         // rocprim temporary storage
@@ -68,6 +69,7 @@ inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int64_t strip_words,
     w.r = (float *)p; p += align256(sizeof(float) * 2 * T);
     w.idx = (int32_t *)p; p += align256(sizeof(int32_t) * T);
     w.order = (int32_t *)p; p += align256(sizeof(int32_t) * T);
+    w.sb = (float *)p; p += align256(sizeof(float) * 4 * T);
     w.removed = (uint64_t *)p; p += align256(sizeof(uint64_t) * sum_nb);
     w.strip = (uint64_t *)p; p += align256(sizeof(uint64_t) * strip_words);
     w.temp = p;
@@ -114,47 +116,84 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
     }
 }
 
-// IoU words of row block ib = s*S + ibl (64 sorted rows) x column block jb >= ib
-__global__ __launch_bounds__(64) void mask_strip_kernel(const int64_t *__restrict__ cand_off,
-                                                        const int64_t *__restrict__ nb_off, double thr,
-                                                        int64_t S, int64_t s, NmsWork w) {
-    __shared__ float jb_box[64][4];
-    __shared__ float jb_area[64];
-    const int jb = blockIdx.x, g = blockIdx.z;
+// Boxes in sorted order, once per call: the strips then read rows and
+// columns contiguously instead of through the order indirection.
+__global__ void sort_boxes_kernel(const int64_t *__restrict__ cand_off, int G, NmsWork w) {
+    const int g = blockIdx.y;
+    const int64_t off = cand_off[g];
+    const int n = (int)(cand_off[g + 1] - off);
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const int li = min(max(w.order[off + p], 0), n - 1);  // NaN-safe
+        reinterpret_cast<float4 *>(w.sb)[off + p] = reinterpret_cast<const float4 *>(w.b)[off + li];
+    }
+}
+
+// IoU words of row block ib = s*S + blockIdx.y (64 sorted rows, one per lane)
+// x column blocks jb0 .. jb0 + NJ - 1 (those >= ib): bit k of word (i, jb) =
+// IoU(row i, column jb*64 + k) > thr for columns after i.  A block of MW
+// waves shares the row block: wave w computes column blocks jb0 + w, jb0 + w
+// + MW, ... with the column boxes staged in LDS (read as broadcasts); the
+// NJ words of each row are then written row-contiguously through an LDS
+// transpose (8 rows x 64 B per store instruction instead of 64 scattered 8-B
+// words per column block), and blocks wholly below the diagonal exit first.
+constexpr int NJ = 8, MW = 4;
+
+__global__ __launch_bounds__(64 * MW) void mask_strip_kernel(const int64_t *__restrict__ cand_off,
+                                                             const int64_t *__restrict__ nb_off, double thr,
+                                                             int64_t S, int64_t s, NmsWork w) {
+    __shared__ float4 cb[NJ * 64];
+    __shared__ float ca[NJ * 64];
+    __shared__ uint64_t tw[64][NJ + 1];
+    const int g = blockIdx.z;
     const int64_t ib = s * S + blockIdx.y;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
-    if (ib >= nb || jb >= nb || jb < ib) return;  // block-uniform
-    const int t = threadIdx.x;
-    const int j = jb * 64 + t;
-    if (j < n) {
-        const int lj = min(max(w.order[off + j], 0), n - 1);  // NaN-safe
-        const float4 bj = reinterpret_cast<const float4 *>(w.b)[off + lj];
-        jb_box[t][0] = bj.x; jb_box[t][1] = bj.y; jb_box[t][2] = bj.z; jb_box[t][3] = bj.w;
-        jb_area[t] = (bj.z - bj.x) * (bj.w - bj.y);
+    const int jb0 = blockIdx.x * NJ;
+    if (ib >= nb || jb0 >= nb || jb0 + NJ <= ib) return;  // block-uniform
+    const int tid = threadIdx.x, t = tid & 63, wv = tid >> 6;
+    const int jlo = max(jb0, (int)ib), jhi = min(jb0 + NJ, nb);  // column blocks of this block
+    const float4 *sb = reinterpret_cast<const float4 *>(w.sb) + off;
+    for (int e = tid; e < (jhi - jlo) * 64; e += 64 * MW) {
+        const int j = jlo * 64 + e;
+        if (j < n) {
+            const float4 bj = sb[j];
+            cb[e] = bj;
+            ca[e] = (bj.z - bj.x) * (bj.w - bj.y);
+        }
     }
     __syncthreads();
     const int i = (int)ib * 64 + t;
-    if (i >= n) return;
-    const int li = min(max(w.order[off + i], 0), n - 1);
-    const float4 bi = reinterpret_cast<const float4 *>(w.b)[off + li];
+    const float4 bi = i < n ? sb[i] : float4{0.0f, 0.0f, 0.0f, 0.0f};
     const float ai = (bi.z - bi.x) * (bi.w - bi.y);
-    uint64_t bits = 0;
-    const int kmax = min(64, n - jb * 64);
-    for (int k = 0; k < kmax; ++k) {
-        if (jb * 64 + k <= i) continue;
-        const float xx1 = fmaxf(bi.x, jb_box[k][0]), yy1 = fmaxf(bi.y, jb_box[k][1]);
-        const float xx2 = fminf(bi.z, jb_box[k][2]), yy2 = fminf(bi.w, jb_box[k][3]);
-        float ww = xx2 - xx1, hh = yy2 - yy1;
-        ww = ww > 0.0f ? ww : 0.0f;
-        hh = hh > 0.0f ? hh : 0.0f;
-        const float inter = ww * hh;
-        const float ovr = inter / (ai + jb_area[k] - inter);
-        if ((double)ovr > thr) bits |= (1ull << k);
+    for (int jb = jlo + wv; jb < jhi; jb += MW) {
+        uint64_t bits = 0;
+        const int kmax = min(64, n - jb * 64);
+        const int kmin = jb == ib ? t + 1 : 0;  // columns after row i only
+        const int base = (jb - jlo) * 64;
+#pragma unroll 4
+        for (int k = 0; k < kmax; ++k) {
+            const float4 bj = cb[base + k];
+            const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+            const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+            float ww = xx2 - xx1, hh = yy2 - yy1;
+            ww = ww > 0.0f ? ww : 0.0f;
+            hh = hh > 0.0f ? hh : 0.0f;
+            const float inter = ww * hh;
+            const float ovr = inter / (ai + ca[base + k] - inter);
+            if (k >= kmin && (double)ovr > thr) bits |= (1ull << k);
+        }
+        tw[t][jb - jb0] = i < n ? bits : 0ull;
     }
-    // strip layout per image: [S*64 rows][nb words]
-    w.strip[S * 64 * nb_off[g] + (int64_t)(blockIdx.y * 64 + t) * nb + jb] = bits;
+    __syncthreads();
+    // strip layout per image: [S*64 rows][nb words]; lanes (8 rows x 8 words)
+    uint64_t *dst = w.strip + S * 64 * nb_off[g] + (int64_t)(blockIdx.y * 64) * nb;
+    const int wq = t & 7, rq = t >> 3;
+    const int jb = jb0 + wq;
+    for (int r0 = 8 * wv; r0 < 64; r0 += 8 * MW) {
+        const int r = r0 + rq;
+        if (jb >= jlo && jb < jhi && (int)ib * 64 + r < n) dst[(int64_t)r * nb + jb] = tw[r][wq];
+    }
 }
 
 // One block of RT threads per image.  Every wave resolves the block's greedy
@@ -295,9 +334,12 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
         hipFuncSetAttribute((const void *)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
         return TMR_E_HIP;
+    hipLaunchKernelGGL(sort_boxes_kernel, dim3((unsigned)std::min<int64_t>(tmr_cdiv(max_cand, 256), 1024), G),
+                       dim3(256), 0, s, cand_off, G, w);
+    TMR_CHECK_LAUNCH();
     for (int64_t st = 0; st * S < max_nb; ++st) {
-        hipLaunchKernelGGL(mask_strip_kernel, dim3((unsigned)max_nb, (unsigned)S, G), dim3(64), 0, s, cand_off,
-                           nb_off, iou_threshold, S, st, w);
+        hipLaunchKernelGGL(mask_strip_kernel, dim3((unsigned)tmr_cdiv(max_nb, NJ), (unsigned)S, G), dim3(64 * MW), 0, s,
+                           cand_off, nb_off, iou_threshold, S, st, w);
         TMR_CHECK_LAUNCH();
         hipLaunchKernelGGL(rk, dim3(G), dim3(RT), lds, s, cand_off, nb_off, S, st, w, out_logits, out_boxes,
                            out_refs, out_keep, kept);
