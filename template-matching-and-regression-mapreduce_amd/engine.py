@@ -63,9 +63,12 @@ class PathConfig:
                    precision=getattr(args, "precision", "fp32"))
 
 
-# Correlation-kernel crossover (tmr_xcorr_algo), from the measured launch
-# times of both kernels per template side k (HIP events, kbench_xcorr,
-# profiles/r02w_sweep{128,192}.jsonl), as ms per unit at the
+# Correlation-kernel crossover (tmr_xcorr_algo).  Since round 3 the table is
+# the committed rocprofv3 sweep (xcorr_cost.json, below): kernel-trace
+# durations of both kernels per k in the two regimes, beside each point's
+# counted HBM bytes and MFMA busy (profiles/xcorr_crossover.json; DESIGN.md
+# 4.3).  The constants here are the round-2 HIP-event tables it replaced
+# (kbench_xcorr, profiles/r02w_sweep{128,192}.jsonl), as ms per unit at the
 # 512 x 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
 # exemplars at 128^2; the image's band staging is shared by 3 units) and
 # E = 16 (8 images x 16 exemplars at 192^2, times / 2.25 for the area).
