@@ -133,6 +133,18 @@ def test_headline_batch_config_d():
     print("config D mean kept per image:", float(np.mean(kept)))
 
 
+def test_config_a_demo_shape():
+    """bench.py config A exactly (1 image, 3 exemplars, k 7..15, cls 0.7, the
+    demo.py thresholds): the detect path vs the oracle forward and its
+    peaks + NMS; the module-API form of the same image is
+    test_demo_infer_call_form's."""
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, 1, 256, 64, 64)
+    ex, _ = synth.exemplar_set(2000, 1, 3, 128, 128, 7, 15)
+    kept = _check_images(P, feats, ex, (0,), 0.7, 0.5, 64)
+    print("config A kept:", kept)
+
+
 def test_config_e_last_image():
     """bench.py config E (8 x 192^2, E = 16, k 3..31): the batch's last image."""
     P = synth.reference_state_dict(0)
