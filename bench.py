@@ -207,6 +207,15 @@ def xcorr_by_class(eng, feats_d, ex, reps: int = 3):
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_by_config.json")
+PEAKS_FILE = os.path.join(REPO, "profiles", "peaks_measured.json")
+
+
+def measured_peaks():
+    """The box's own peaks (profiles/peakbench), or None."""
+    if not os.path.exists(PEAKS_FILE):
+        return None
+    with open(PEAKS_FILE) as fh:
+        return json.load(fh)
 
 
 def load_pmc(config: str, role: str):
@@ -464,6 +473,17 @@ def main():
                      "2*C*(H-h+1)(W-w+1)*h*w FLOPs (SURVEY.md 8d)"}
         if not a.no_xcorr_classes:
             out["roofline_xcorr"]["by_class"] = xcorr_by_class(eng, feats_d, ex)
+        mp = measured_peaks()
+        if mp:  # fractions of the peaks measured on an MI355X (the datasheet ones stay `peak`)
+            mk = "mfma_bf16_tflops" if prec == "bf16" else "mfma_f16_tflops"
+            out["roofline"]["peak_measured"] = mp.get(mk)
+            out["roofline"]["frac_of_measured_peak"] = round(alg_achieved / mp[mk], 4) if mp.get(mk) else None
+            out["roofline"]["executed_frac_of_measured_peak"] = \
+                round(executed_achieved / mp[mk], 4) if mp.get(mk) else None
+            out["roofline_xcorr"]["hbm_measured_gbs"] = mp.get("hbm_copy_gbs")
+            out["roofline_xcorr"]["dram_min_frac_of_measured"] = \
+                round(xc_dram / xs / 1e9 / mp["hbm_copy_gbs"], 4) if mp.get("hbm_copy_gbs") else None
+            out["peaks_measured_source"] = mp.get("source", "profiles/peaks_measured.json")
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(P, feats, ex, a.cpu_seconds, cfg["cls"], cfg["iou"])
         else:

@@ -1,5 +1,5 @@
 # r03k: round-3 end-of-session check of the tree: full -m gpu suite (incl. the config A/C/D
-# graded-batch tests), smoke(), bench lines of every config (B with the default K/W and CPU
+# graded-batch tests), the box's peaks (peakbench), smoke(), bench lines of every config (B with the default K/W and CPU
 # baseline), rocprofv3 kernel traces of B, C and E, and the --gpus 2 launcher over gloo.
 # Run from the repo root: gpurun -- bash profiles/gpu_r03k.sh
 set -o pipefail
@@ -8,6 +8,9 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/r03k_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r03k_gpu_tests.log; exit 1; }
 tail -1 gpurun_out/r03k_gpu_tests.log
 grep -E "worst normwise map error|mean kept|config A kept" gpurun_out/r03k_gpu_tests.log
+timeout -k 10 120 ./profiles/peakbench/peakbench > gpurun_out/r03k_peaks.json 2> gpurun_out/r03k_peaks.err || { cat gpurun_out/r03k_peaks.err; exit 1; }
+cat gpurun_out/r03k_peaks.json
+python -c "import json;d=json.load(open('gpurun_out/r03k_peaks.json'));d['source']='profiles/peakbench (round r03k box)';json.dump(d,open('profiles/peaks_measured.json','w'),indent=1)" || exit 1
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r03k_smoke.log 2>&1 || { tail -20 gpurun_out/r03k_smoke.log; exit 1; }
 tail -1 gpurun_out/r03k_smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/r03k_bench_B.json 2> gpurun_out/r03k_bench_B.err || exit 1
