@@ -402,6 +402,9 @@ def main():
         xc_flops, xc_bytes, xc_dram = eng.last_xcorr_flops, eng.last_xcorr_bytes, eng.last_xcorr_dram_bytes
         pmc_heads = load_pmc(a.config, "heads") if own_options else None
         pmc_xc = load_pmc(a.config, "xcorr") if own_options else None
+        if pmc_xc and pmc_xc.get("kernel_names") and not any(
+                ("rows" if eng.last_xcorr_algo == "valu" else "mfma") in n for n in pmc_xc["kernel_names"]):
+            pmc_xc = None  # the PMC run measured the other correlation kernel
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),

@@ -36,22 +36,25 @@ def collect(kernel, paths):
     vals = collections.defaultdict(list)
     dur = []
     seen = set()
+    names = set()
     for f, row in rows:
         if int(row["Grid_Size"]) != gmax:
             continue
+        names.add(row["Kernel_Name"])
         vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
         key = (f, row["Dispatch_Id"])
         if key not in seen:
             seen.add(key)
             dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    collect.names = sorted(names)
     return vals, dur
 
 
 def summarize(kernel, paths):
     vals, dur = collect(kernel, paths)
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"kernel": kernel, "launches": {k: len(v) for k, v in vals.items()},
-           "counters": avg}
+    res = {"kernel": kernel, "kernel_names": getattr(collect, "names", []),
+           "launches": {k: len(v) for k, v in vals.items()}, "counters": avg}
     if dur:
         res["avg_launch_s"] = sum(dur) / len(dur)
     if "FETCH_SIZE" in avg:

@@ -71,9 +71,11 @@ def all_gather_detections(counts: torch.Tensor, rows: torch.Tensor, group=None):
     world = dist.get_world_size(group)
     dev = rows.device
     nimg = torch.tensor([counts.numel(), rows.shape[0]], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(nimg) for _ in range(world)]
-    dist.all_gather(sizes, nimg, group=group)
-    sizes = torch.stack(sizes).cpu().numpy()
+    # one contiguous receive buffer per collective (all_gather_into_tensor:
+    # RCCL writes every rank's block in place, no per-rank tensors to stack)
+    sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, nimg, group=group)
+    sizes = sizes.view(world, 2).cpu().numpy()
     # payload rows: ceil(images / ROW) rows of counts, then the detection rows
     crow = -(-sizes[:, 0] // ROW)
     pmax = int((crow + sizes[:, 1]).max())
@@ -82,8 +84,9 @@ def all_gather_detections(counts: torch.Tensor, rows: torch.Tensor, group=None):
     if counts.numel():
         pad.view(-1)[:counts.numel()] = counts.to(torch.int32).view(torch.float32)
     pad[nc:nc + rows.shape[0]] = rows
-    got = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(got, pad, group=group)
+    got = torch.empty((world * pad.shape[0], ROW), dtype=pad.dtype, device=dev)
+    dist.all_gather_into_tensor(got, pad, group=group)
+    got = got.view(world, pad.shape[0], ROW)
     g_counts = torch.cat([got[r].view(-1)[:int(sizes[r, 0])].view(torch.int32) for r in range(world)])
     g_rows = torch.cat([got[r][int(crow[r]):int(crow[r]) + int(sizes[r, 1])] for r in range(world)])
     return g_counts, g_rows
