@@ -516,7 +516,10 @@ class TMREngine:
     # ------------------------------------------------------------ forward
     def _feat_absmax(self, feats: torch.Tensor) -> torch.Tensor:
         """max(1, max |feats|) as a device scalar (memoised per tensor): the
-        scale source of the [up2x(f); 1] records (bilinear weights are convex)."""
+        scale source of the [up2x(f); 1] records (bilinear weights are convex).
+        None under the bf16 contract: bf16 records and kernels are unscaled."""
+        if self.cfg.precision == "bf16":
+            return None
         return self._memo_absmax(feats, "feat", lambda: absmax(
             feats, torch.ones(1, device=feats.device, dtype=torch.float32)))
 
@@ -707,7 +710,8 @@ class TMREngine:
                 # records of [up2x(f); 1] (max |.| <= max(max|f|, 1): bilinear
                 # weights are convex); one activation scale per conv launch
                 xmax0 = self._feat_absmax(feats)
-                tm_max = self._memo_absmax(f_tm, "ftm", lambda: absmax(f_tm))
+                unscaled = cfg.precision == "bf16"  # no activation scales (bf16 records)
+                tm_max = None if unscaled else self._memo_absmax(f_tm, "ftm", lambda: absmax(f_tm))
                 if share:
                     # the fp half is its own launch (tmr_split_conv_store) with
                     # its own activation scale
@@ -719,7 +723,7 @@ class TMREngine:
                     # ONE launch reads both sources and undoes ONE activation
                     # scale (conv_split.hip takes one xmax per launch): both
                     # record sets are packed with max(max|f_TM|, xmax0)
-                    xmax1 = absmax(tm_max, xmax0.clone())
+                    xmax1 = None if unscaled else absmax(tm_max, xmax0.clone())
                     xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax1,
                                         ones=False)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
