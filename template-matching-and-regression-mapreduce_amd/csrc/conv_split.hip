@@ -66,7 +66,13 @@ typedef __attribute__((address_space(3))) void *lds_ptr_t;
 // r02an), wave priority over the MFMA stream (no change, r02av).
 
 constexpr int BM = 128;      // output channels per block
-constexpr int TH = 16;       // output rows per block
+#ifndef TMR_SPLIT_TH  // output rows per block (8: with TMR_SPLIT_NW=4 and a halved LDS budget, two
+#define TMR_SPLIT_TH 16 // co-resident blocks per CU, measured as a variant: DESIGN.md 4.2)
+#endif
+#ifndef TMR_SPLIT_LDS_KB  // LDS budget per block
+#define TMR_SPLIT_LDS_KB 160
+#endif
+constexpr int TH = TMR_SPLIT_TH;
 constexpr int TW = 32;       // output cols per block
 // waves per block: 8 (2 along n x 4 along rows, 128 accumulator VGPRs, two
 // waves per SIMD) or 4 (1 x 4, 256 accumulators, one wave per SIMD: half
@@ -94,7 +100,8 @@ constexpr int TW = 32;       // output cols per block
 #endif
 constexpr int NWAVES = TMR_SPLIT_NW;
 constexpr int NTHREADS = NWAVES * 64;
-constexpr int WNS = NWAVES == 8 ? 2 : 1;  // waves along n
+constexpr int WNS = (NWAVES == 8 || TH == 8) ? 2 : 1;  // waves along n
+static_assert(TH == 4 * NWAVES / WNS, "a wave owns 4 output rows");
 constexpr int NIN = 8 / WNS;              // 16-channel n fragments per wave
 constexpr int ACCW = NIN * 8 * 64 * 4;    // accumulator floats per wave
 constexpr int NHEAD = 5;
@@ -211,7 +218,10 @@ struct Geo {
     static constexpr int HB = MPW * NWAVES * 1024;
     static constexpr int NPLW = Prec<PREC>::WREC / 16;         // weight planes per tap (8 or 4)
     static constexpr int WB1 = NPLW * WPL;                     // weight bytes per tap
-    static constexpr bool fits(int tps, int nwb) { return 2 * HB + nwb * tps * WB1 <= 160 * 1024; }
+    // (a reduced budget applies to the 3x3 decoders; larger kernels keep the CU's 160 KB)
+    static constexpr bool fits(int tps, int nwb) {
+        return 2 * HB + nwb * tps * WB1 <= (KS <= 3 ? TMR_SPLIT_LDS_KB : 160) * 1024;
+    }
     // taps per barrier step and weight buffers (DMA lookahead NWB-1 steps)
     static constexpr int TPS = T == 1 ? 1 : fits(3, 2) ? 3 : fits(2, 2) ? 2 : 1;
     static constexpr int NWB = fits(TPS, 3) ? 3 : 2;
