@@ -15,6 +15,7 @@ counts bit-exact given the GPU's own maps; the end-to-end agreement with the
 oracle's maps is reported (oracle/agreement.py) and held to its contract.
 """
 import json
+import os
 from types import SimpleNamespace
 
 import numpy as np
@@ -72,7 +73,6 @@ def _check_images(P, feats, ex, images, thr, iou, hf, precision="fp32", tol=TOL)
     ui = np.repeat(np.arange(B), E)
     r = eng.forward_units(fd, ui, ex.reshape(-1, 4))
     o, b = r["o"].cpu().numpy(), r["b"].cpu().numpy()
-    lines = []
     worst = 0.0
     for img in images:
         units = [img * E + e for e in range(E)]
@@ -95,8 +95,7 @@ def _check_images(P, feats, ex, images, thr, iou, hf, precision="fp32", tol=TOL)
         rep = agreement.compare(omaps, gmaps, list(ex[img]), thr, iou)
         if precision == "fp32":
             agreement.check(rep)
-        lines.append(agreement.report_line(f"image {img} oracle-maps vs GPU-maps ({precision}):", rep))
-    print("\n".join(lines))
+        print(agreement.report_line(f"image {img} oracle-maps vs GPU-maps ({precision}):", rep), flush=True)
     print(f"{precision} worst normwise map error over the checked units: {worst:.2e} (contract {tol:g})")
     return [int(x.shape[0]) for x in L]
 
@@ -131,6 +130,29 @@ def test_headline_batch_config_d():
     ex, _ = synth.exemplar_set(2000, 64, 1, 128, 128, 3, 15)
     kept = _check_images(P, feats, ex, (0, 63), 0.4, 0.5, 64)
     print("config D mean kept per image:", float(np.mean(kept)))
+
+
+FULL_BATCH = {  # bench.py's configs: (images, E, feature side, k range, precision, tol, cls threshold)
+    "B": (64, 3, 64, (3, 15), "fp32", TOL, 0.1),
+    "C": (64, 3, 64, (3, 15), "bf16", 1e-2, 0.25),
+    "D": (64, 1, 64, (3, 15), "fp32", TOL, 0.4),
+    "E": (8, 16, 96, (3, 31), "fp32", TOL, 0.1),
+}
+
+
+@pytest.mark.skipif(not os.environ.get("TMR_FULL_PARITY"),
+                    reason="every image of the batch against the oracle (~1 s of CPU per unit); "
+                           "set TMR_FULL_PARITY=1 (record: profiles/r03p_full_parity.log)")
+@pytest.mark.parametrize("config", sorted(FULL_BATCH))
+def test_full_batch_every_image(config):
+    """bench.py configs B, C, D and E with EVERY image of the batch checked
+    like the headline tests check images 0 / 31 / 63."""
+    nb, E, hf, (k0, k1), precision, tol, thr = FULL_BATCH[config]
+    P = synth.reference_state_dict(0)
+    feats = synth.sam_features(1000, nb, 256, hf, hf)
+    ex, _ = synth.exemplar_set(2000, nb, E, 2 * hf, 2 * hf, k0, k1)
+    kept = _check_images(P, feats, ex, range(nb), thr, 0.5, hf, precision=precision, tol=tol)
+    print(f"config {config} all {nb} images: mean kept per image {float(np.mean(kept))}")
 
 
 def test_config_a_demo_shape():
