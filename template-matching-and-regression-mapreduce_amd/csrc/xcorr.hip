@@ -673,9 +673,6 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
 // row 0), issued PF template rows ahead of their MFMAs.  (Measured: staging
 // them through an LDS table per row chunk, with its two barriers per chunk,
 // was slower at every k >= 11; profiles/r02b_kbench_xcorr_*.)
-#ifndef TMR_XCORR_BRING  // B fragments through a register ring (see mfma_unit)
-#define TMR_XCORR_BRING 0
-#endif
 template <int NTW, int NK, int WPR, int PM>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
@@ -686,69 +683,6 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
     auto afrag = [&](int i, int nk, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
     };
-#if TMR_XCORR_BRING
-    // The row's NS = NK * NTW B fragments (element s: K block s / NTW, tile
-    // s % NTW) pass through a ring of R register slots, each read R - 1
-    // elements before its MFMAs, across template-row boundaries (R divides
-    // NS, so element s of every row sits in slot s % R).  Left to itself the
-    // compiler reads each tile's fragment right before its MFMAs and waits
-    // out the LDS latency once per tile (lgkmcnt(0) every 3 MFMAs).
-    constexpr int NS = NK * NTW;
-    constexpr int R = NS % 4 == 0 ? 4 : NS % 3 == 0 ? 3 : NS % 2 == 0 ? 2 : 1;
-    V rh[R], rl[R];
-    auto bread = [&](int i, int s, int slot) {
-        const int nk = s / NTW, t = s % NTW;
-        const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-        rh[slot] = *reinterpret_cast<const V *>(Fh + (size_t)(rb + i) * SB + colb);
-        if (SPLIT) rl[slot] = *reinterpret_cast<const V *>(Fl + (size_t)(rb + i) * SB + colb);
-    };
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < h) {
-#pragma unroll
-            for (int nk = 0; nk < NK; ++nk) {
-                ah[p][nk] = afrag(p, nk, 0);
-                if (SPLIT) al[p][nk] = afrag(p, nk, 1);
-            }
-        }
-#pragma unroll
-    for (int s = 0; s < R - 1; ++s) bread(0, s, s);
-    for (int i0 = 0; i0 < h; i0 += PF) {
-#pragma unroll
-        for (int p = 0; p < PF; ++p) {
-            const int i = i0 + p;
-            if (i >= h) break;
-            V ch[NK], cl[NK];
-#pragma unroll
-            for (int nk = 0; nk < NK; ++nk) {
-                ch[nk] = ah[p][nk];
-                if (SPLIT) cl[nk] = al[p][nk];
-            }
-            if (i + PF < h) {
-#pragma unroll
-                for (int nk = 0; nk < NK; ++nk) {
-                    ah[p][nk] = afrag(i + PF, nk, 0);
-                    if (SPLIT) al[p][nk] = afrag(i + PF, nk, 1);
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                const int sp = s + R - 1;  // the element read now (slot sp % R)
-                if (sp < NS)
-                    bread(i, sp, sp % R);
-                else  // the next row's (the last row re-reads itself: no branch)
-                    bread(min(i + 1, h - 1), sp - NS, sp % R);
-                const int nk = s / NTW, t = s % NTW;
-                acc[t] = xmma(ch[nk], rh[s % R], acc[t]);
-                if (SPLIT) {
-                    acc[t] = xmma(ch[nk], rl[s % R], acc[t]);
-                    acc[t] = xmma(cl[nk], rh[s % R], acc[t]);
-                }
-            }
-        }
-    }
-    return;
-#endif
 #pragma unroll
     for (int p = 0; p < PF; ++p)
         if (p < h) {
