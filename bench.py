@@ -276,6 +276,8 @@ def main():
     prec = a.precision or cfg.get("precision", "fp32")
     eng = tmr.TMREngine(P, tmr.PathConfig(precision=prec))
     eng.decoder_algo = a.decoder
+    # A/B knob: TMR_BENCH_OUT_BF16=0 keeps the bf16 contract's f_TM plane in fp32
+    eng.out_bf16 = os.environ.get("TMR_BENCH_OUT_BF16", "1") != "0"
     B = a.batch or cfg["batch"]
     E = a.exemplars or cfg["E"]
     feats = synth.sam_features(1000 + rank, B, CIN, H // 2, W // 2)

@@ -145,6 +145,19 @@ int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *temp
                    const float *scale, int squeeze, float *out, float *relu_out, float *work,
                    float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
                    int min_k, int prec, void *stream);
+/* tmr_xcorr_prec with the f_TM plane's element type chosen: out_bf16 = 0 is
+ * tmr_xcorr_prec (out float [U][C][H][W]); out_bf16 = 1 writes out as bf16
+ * [U][C][H][W], each element the round-to-nearest-even bf16 of the fp32
+ * value tmr_xcorr_prec would write -- the bf16 contract's detect path, whose
+ * decoder records (tmr_split_xpack16) are those bf16 values.  out_bf16 needs
+ * algo TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0 and relu_out NULL
+ * (TMR_E_INVALID otherwise).  Same sources as tmr_xcorr_prec:
+ * models/template_matching.py:23-41,97. */
+int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
+                  const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
+                  const float *scale, int squeeze, void *out, float *relu_out, float *work,
+                  float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
+                  int min_k, int prec, int out_bf16, void *stream);
 /* Operand prep of the MFMA correlation: per (unit u, channel c) template
  * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
  * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <
@@ -240,6 +253,11 @@ int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stre
 int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec);
 int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
                     const float *xmax, void *out, void *stream);
+/* tmr_split_xpack16: the TMR_PREC_BF16 records of a bf16 x [S][C][H][W]
+ * (tmr_xcorr_out's bf16 f_TM; W % 8 == 0): bit-identical to tmr_split_xpack
+ * of the fp32 values those bf16 elements round. */
+int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
+                      void *stream);
 /* tmr_split_xpack_up: records of [up2x(f) (upsample) or f; 1 (ones)] from the
  * SAM features f [S][Cin][Hin][Win] (sizes: tmr_split_xpack_size with
  * C = Cin + ones at the output resolution).  With tmr_split_fold_proj it

@@ -66,6 +66,8 @@ SIGNATURES = {
                             _I, _I, _P]),
     "tmr_xcorr_prec": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
                             _I, _I, _I, _P]),
+    "tmr_xcorr_out": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
+                           _I, _I, _I, _I, _P]),
     "tmr_template_split_size": (_L, [_I, _I, _L]),
     "tmr_template_split": (_I, [_P, _P, _I, _I, _L, _P, _P]),  # (..., total_rows, out, stream)
     "tmr_template_split_prec": (_I, [_P, _P, _I, _I, _L, _I, _P, _P]),  # (..., total_rows, prec, out, stream)
@@ -80,6 +82,7 @@ SIGNATURES = {
     "tmr_absmax": (_I, [_P, _L, _I, _P, _P]),
     "tmr_split_xpack_size": (_L, [_I, _I, _I, _I, _I, _I]),
     "tmr_split_xpack": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_xpack16": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "tmr_split_xpack_up": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "tmr_split_fold_proj": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "tmr_split_wpack_size": (_L, [_I, _I, _I, _I, _I]),

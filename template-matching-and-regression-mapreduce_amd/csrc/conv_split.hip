@@ -887,15 +887,19 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
 #define TMR_XPACK4_3T 0
 #endif
 constexpr int XSEG = TMR_XSEG;
-template <int PREC>
-__global__ __launch_bounds__(256) void xpack4_kernel(const float *__restrict__ x, int S, int Cin, int H, int W,
+// IN: the activation's element type, float or __bf16 (a bf16 f_TM plane from
+// tmr_xcorr_out: bf16 records of it are its own elements, tmr_split_xpack16)
+template <int PREC, typename IN = float>
+__global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, int S, int Cin, int H, int W,
                                                      int NCc, int Hp, int Wp, int pad, int64_t nseg,
                                                      int64_t nbord, const float *__restrict__ xmax,
                                                      typename Prec<PREC>::V *__restrict__ out) {
     constexpr int HALVES = Prec<PREC>::HALVES;
     typedef typename Prec<PREC>::V V;
     typedef typename Prec<PREC>::E E;
-    __shared__ float tile[CCH][XSEG];
+    constexpr int VE = 16 / sizeof(IN);  // elements per 16-B load
+    typedef IN INV __attribute__((ext_vector_type(VE)));
+    __shared__ __attribute__((aligned(16))) IN tile[CCH][XSEG];
     const size_t plane = (size_t)Hp * Wp;
     const int t = threadIdx.x;
     if ((int64_t)blockIdx.x < nseg) {
@@ -907,15 +911,15 @@ __global__ __launch_bounds__(256) void xpack4_kernel(const float *__restrict__ x
         r /= H;
         const int c = (int)(r % NCc);
         const int s = (int)(r / NCc);
-        const int x0 = sx * XSEG, nx = min(XSEG, W - x0);  // nx % 4 == 0
-        const float *src = x + ((size_t)s * Cin + (size_t)c * CCH) * H * W + (size_t)y * W + x0;
+        const int x0 = sx * XSEG, nx = min(XSEG, W - x0);  // nx % VE == 0
+        const IN *src = x + ((size_t)s * Cin + (size_t)c * CCH) * H * W + (size_t)y * W + x0;
 #pragma unroll
-        for (int k = 0; k < CCH * XSEG / 4 / 256; ++k) {
-            const int e = t + 256 * k, ch = e / (XSEG / 4), x4 = e % (XSEG / 4);
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (4 * x4 < nx && c * CCH + ch < Cin)
-                v = *reinterpret_cast<const float4 *>(src + (size_t)ch * H * W + 4 * x4);
-            *reinterpret_cast<float4 *>(&tile[ch][4 * x4]) = v;
+        for (int k = 0; k < CCH * XSEG / VE / 256; ++k) {
+            const int e = t + 256 * k, ch = e / (XSEG / VE), xv = e % (XSEG / VE);
+            INV v = {};
+            if (VE * xv < nx && c * CCH + ch < Cin)
+                v = *reinterpret_cast<const INV *>(src + (size_t)ch * H * W + VE * xv);
+            *reinterpret_cast<INV *>(&tile[ch][VE * xv]) = v;
         }
         __syncthreads();
         const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
@@ -927,7 +931,7 @@ __global__ __launch_bounds__(256) void xpack4_kernel(const float *__restrict__ x
                 V hi, lo;
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {  // split_record's arithmetic
-                    const float xs = tile[q * 8 + m][px] * sc;
+                    const float xs = (float)tile[q * 8 + m][px] * sc;
                     const E h = (E)xs;
                     hi[m] = h;
                     if (HALVES == 2) lo[m] = (E)(xs - (float)h);
@@ -1153,6 +1157,20 @@ extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int k
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
     return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, out, stream);
+}
+
+extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
+                                 void *stream) {
+    TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec == TMR_PREC_BF16);
+    TMR_REQUIRE(W % 8 == 0);
+    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
+    const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
+    hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16, __bf16>), g4, dim3(256), 0, tmr_stream(stream),
+                       static_cast<const __bf16 *>(x), S, C, H, W, NCc, Hp, Wp, ks / 2, nseg, nbord, nullptr,
+                       static_cast<b8 *>(out));
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
 }
 
 extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample,

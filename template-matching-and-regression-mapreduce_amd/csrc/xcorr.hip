@@ -729,7 +729,10 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
     }
 }
 
-template <int NTW, int NV4, int TRB, int PM>
+// OB: f_TM leaves as bf16 (the bf16 contract's detect path: the decoder's
+// bf16 records are bf16(f_TM) either way, so the fp32 plane is never needed;
+// half the bytes written here and read by the record pack)
+template <int NTW, int NV4, int TRB, int PM, bool OB = false>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
@@ -831,7 +834,9 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;
-        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane : outp + ((size_t)u * a.C + c) * plane;
+        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
+                    : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)u * a.C + c) * plane)
+                         : outp + ((size_t)u * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         const int y = yb0 + tr * 16 + l16;
         if (row_live && y < yb1) {
@@ -845,6 +850,11 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                     const int xx = x + j;
                     r4[j] = (vy && xx >= pw && xx < pw + Wo) ? div_cr(acc[t][j] * inv, denom, rden) * sc : 0.0f;
                     vmax = fmaxf(vmax, fabsf(r4[j]));
+                }
+                if (OB) {
+                    *reinterpret_cast<b4 *>(reinterpret_cast<__bf16 *>(op) + (size_t)y * W + x) =
+                        b4{(__bf16)r4[0], (__bf16)r4[1], (__bf16)r4[2], (__bf16)r4[3]};
+                    continue;
                 }
                 *reinterpret_cast<float4 *>(op + (size_t)y * W + x) = float4{r4[0], r4[1], r4[2], r4[3]};
                 if (rp)
@@ -911,28 +921,28 @@ static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
     return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
 }
 
-template <int NTW, int NV4, int TRB, int PM>
+template <int NTW, int NV4, int TRB, int PM, bool OB>
 static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp) {
-    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM>;
+    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return TMR_E_HIP;
-    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
                        texp, a.out, a.units);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
 
-template <int TRB, int PM>
+template <int TRB, int PM, bool OB = false>
 static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp, int nv4) {
     const int ntw = a.W / 16 / (4 / TRB);
     switch (ntw) {
-#define TMR_NTW(K)                                                                         \
-    case K:                                                                                \
-        return nv4 == 8 ? launch_mfma_t<K, 8, TRB, PM>(a, m, lds, nblk, s, trows, texp)    \
-                        : launch_mfma_t<K, 16, TRB, PM>(a, m, lds, nblk, s, trows, texp);
+#define TMR_NTW(K)                                                                             \
+    case K:                                                                                    \
+        return nv4 == 8 ? launch_mfma_t<K, 8, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp)    \
+                        : launch_mfma_t<K, 16, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp);
         TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8)
 #undef TMR_NTW
         default: return TMR_E_UNSUPPORTED;
@@ -940,7 +950,7 @@ static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
 }
 
 static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, int max_wt,
-                       const void *tmpl_split, int64_t total_rows, int prec) {
+                       const void *tmpl_split, int64_t total_rows, int prec, bool out16) {
     MArgs m;
     // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
     // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*)
@@ -961,6 +971,9 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
                                                             (int64_t)a.C * total_rows * 2 * AFRAG);
     (void)U;
     const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
+    if (out16)
+        return prec == TMR_PREC_BF16 ? launch_mfma_w<2, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp, nv4)
+                                     : TMR_E_UNSUPPORTED;
     switch (prec) {
         case TMR_PREC_F16X3: return launch_mfma_w<2, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
         case TMR_PREC_BF16: return launch_mfma_w<2, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
@@ -993,12 +1006,15 @@ extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *unit
     return tmr_template_split_prec(templates, units, U, C, total_rows, TMR_PREC_F16X3, out, stream);
 }
 
-extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
-                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                              float *work, float *out_absmax, const void *tmpl_split,
-                              int64_t total_rows, int algo, int min_k, int prec, void *stream) {
+extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
+                             const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                             int max_wt, const float *scale, int squeeze, void *out, float *relu_out,
+                             float *work, float *out_absmax, const void *tmpl_split,
+                             int64_t total_rows, int algo, int min_k, int prec, int out_bf16,
+                             void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
+    // a bf16 f_TM plane: the one-term bf16 MFMA kernel only, no relu / squeeze outputs
+    TMR_REQUIRE(!out_bf16 || (algo == TMR_XCORR_MFMA && prec == TMR_PREC_BF16 && !squeeze && !relu_out));
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
     TMR_REQUIRE(!squeeze || work);
     TMR_REQUIRE(algo >= TMR_XCORR_AUTO && algo <= TMR_XCORR_MFMA);
@@ -1009,7 +1025,7 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
     a.units = units;
     a.img_units = img_units;
     a.scale = scale;
-    a.out = out;
+    a.out = static_cast<float *>(out);  // bf16 elements when out_bf16
     a.relu_out = relu_out;
     a.work = work;
     a.out_absmax = reinterpret_cast<unsigned *>(out_absmax);
@@ -1023,7 +1039,7 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
     if (algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
     const bool use_mfma = algo == TMR_XCORR_MFMA || (algo == TMR_XCORR_AUTO && fits && min_k >= kMfmaMinK);
     if (use_mfma) {
-        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows, prec);
+        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows, prec, out_bf16 != 0);
         if (rc != TMR_OK) return rc;
     } else {
         // row-tiled kernel when rows are 16-B aligned and templates fit its
@@ -1057,11 +1073,20 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
     if (squeeze) {
         int64_t tot = (int64_t)U * H * W;
         hipLaunchKernelGGL(xcorr_squeeze_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, s,
-                           work, units, U, C, H, W, scale, out, relu_out,
+                           work, units, U, C, H, W, scale, a.out, relu_out,
                            reinterpret_cast<unsigned *>(out_absmax));
         TMR_CHECK_LAUNCH();
     }
     return TMR_OK;
+}
+
+extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
+                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
+                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
+                              float *work, float *out_absmax, const void *tmpl_split,
+                              int64_t total_rows, int algo, int min_k, int prec, void *stream) {
+    return tmr_xcorr_out(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
+                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, stream);
 }
 
 extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,

@@ -213,6 +213,8 @@ def pack_wino(w: torch.Tensor) -> torch.Tensor:
 def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """max |x| as a 1-element device tensor (max(out, |x|) when out is given)."""
     require_gpu(x, "absmax input")
+    if x.dtype != torch.float32:
+        raise TMRError(f"absmax of a {x.dtype} tensor (fp32 only)")
     x = x.contiguous()
     acc = out is not None
     if out is None:
@@ -246,15 +248,21 @@ def pack_split_w(w: torch.Tensor, c0: int, precision: str):
 
 
 def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -> torch.Tensor:
-    """[S,C,H,W] fp32 -> zero-padded 16-bit records (tmr_split_xpack)."""
+    """[S,C,H,W] fp32 -> zero-padded 16-bit records (tmr_split_xpack); a bf16
+    x (the correlation's bf16 f_TM plane, tmr_xcorr_out) under the bf16
+    contract -> the same records (tmr_split_xpack16)."""
     require_gpu(x, "conv input")
-    x = x.float().contiguous()
     S, C, H, W = x.shape
     pc = prec_code(precision)
     n = load().tmr_split_xpack_size(S, C, H, W, ks, pc)
     if n <= 0:
         raise TMRError(f"unsupported conv input {tuple(x.shape)}")
     out = torch.empty(n, device=x.device, dtype=torch.uint8)
+    if x.dtype == torch.bfloat16:
+        x = x.contiguous()
+        call("tmr_split_xpack16", ptr(x), S, C, H, W, ks, pc, ptr(out), stream())
+        return out
+    x = x.float().contiguous()
     call("tmr_split_xpack", ptr(x), S, C, H, W, ks, pc, ptr(xmax), ptr(out), stream())
     return out
 
@@ -378,6 +386,10 @@ class TMREngine:
         # "valu" or "mfma" (csrc/xcorr.hip)
         self.xcorr_algo = "auto"
         self.last_xcorr_algo = None
+        # bf16 contract, detect path: the one-term MFMA correlation writes
+        # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
+        self.out_bf16 = True
+        self.last_xcorr_out16 = False
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
@@ -601,8 +613,11 @@ class TMREngine:
         return fp, f0
 
     def match(self, fp: torch.Tensor, unit_image: Sequence[int], unit_boxes: np.ndarray,
-              want_relu: bool = False):
-        """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu)."""
+              want_relu: bool = False, allow_bf16: bool = False):
+        """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu).
+        allow_bf16: the caller only packs f_TM into bf16 decoder records (the
+        bf16 contract's detect path), so the one-term bf16 MFMA kernel may
+        write it as bf16 (tmr_xcorr_out; the records are bit-identical)."""
         B, C, H, W = fp.shape
         U = len(unit_image)
         cfg = self.cfg
@@ -614,8 +629,6 @@ class TMREngine:
         tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
         call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
         Co = 1 if cfg.squeeze else C
-        out = torch.empty((U, Co, H, W), device=dev, dtype=torch.float32)
-        relu = torch.empty_like(out) if want_relu else None
         work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
         scale = self.P["matcher.scale"].detach().float().contiguous()
         # max |f_TM| fused in the kernel: per-workgroup maxima into 256 slots
@@ -635,16 +648,21 @@ class TMREngine:
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
+        out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
+                 and not cfg.squeeze and not want_relu and W % 8 == 0)
+        self.last_xcorr_out16 = out16
+        out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
+        relu = torch.empty_like(out) if want_relu else None
         tsplit = None
         if algo != XCORR_ALGOS["valu"] and tfl > 0:
             # the MFMA correlation's template operands (per (unit, channel) scale)
             rows = host.tsplit_rows(units)
             tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
             call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
-        call("tmr_xcorr_prec", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+        call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
              mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
              ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
-             rows if tsplit is not None else 0, algo, min_k, pc, stream())
+             rows if tsplit is not None else 0, algo, min_k, pc, int(out16), stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
@@ -730,14 +748,16 @@ class TMREngine:
                 C0k = C0
             elif splitk:
                 # 16-bit operand records; one activation scale per conv launch
-                # (both sources of a virtual concat share it)
+                # (both sources of a virtual concat share it); bf16 records
+                # are unscaled (no reductions; f_TM may be a bf16 plane)
+                unscaled = cfg.precision == "bf16"
                 if share:
-                    xmax0 = absmax(fp)
+                    xmax0 = None if unscaled else absmax(fp)
                     xp0 = pack_split_x(fp, ks, cfg.precision, xmax0)
-                    xmax1 = absmax(f_tm)
+                    xmax1 = None if unscaled else absmax(f_tm)
                 else:
-                    xmax1 = absmax(fp) if src0 is not None else None
-                    xmax1 = absmax(f_tm, xmax1)
+                    xmax1 = absmax(fp) if src0 is not None and not unscaled else None
+                    xmax1 = None if unscaled else absmax(f_tm, xmax1)
                     xp0 = pack_split_x(fp, ks, cfg.precision, xmax1) if src0 is not None else None
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
             if share:
@@ -864,7 +884,11 @@ class TMREngine:
             f_tm = fp.index_select(0, ui).contiguous()
             relu = torch.relu(f_tm) if want_aux else None
         else:
-            f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux)
+            # a bf16 f_TM plane only where the decode packs it into bf16
+            # records and nothing else reads it
+            split1 = self.decoder_algo == "split" and self.cfg.decoder_num_layer == 1
+            f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux,
+                                    allow_bf16=split1 and not want_aux)
         o, b = self.decode(fp, f_tm, unit_image, feats)
         return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
 

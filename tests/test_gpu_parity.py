@@ -351,6 +351,13 @@ def test_xpack_records_bitexact(S, C, H, W, ks):
         assert got.numel() == ref.numel(), prec
         bad = int((got != ref).sum())
         assert bad == 0, f"{prec}: {bad} of {ref.numel()} 16-bit words differ"
+        if prec == "bf16" and W % 8 == 0:
+            # the bf16 input form (tmr_split_xpack16 of bf16(x), the bf16
+            # f_TM plane of tmr_xcorr_out): the same records bit for bit
+            out16 = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
+            xb = x.to(torch.bfloat16)
+            call("tmr_split_xpack16", ptr(xb), S, C, H, W, ks, PREC_CODES[prec], ptr(out16), stream())
+            assert torch.equal(out16, out), "xpack16"
 
 
 def test_split_acc_slab_bf16():
@@ -794,6 +801,20 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
         outs[algo] = got
         assert amax.max().item() == np.abs(got).max(), algo
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0)), algo
+        if algo == "mfma" and prec == "bf16":
+            # tmr_xcorr_out's bf16 plane: RNE bf16 of the fp32 plane, bit for bit
+            o16 = torch.empty((U, C, H, W), device=DEV, dtype=torch.bfloat16)
+            call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
+                 ptr(o16), None, None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, 1, stream())
+            torch.cuda.synchronize()
+            assert torch.equal(o16.view(torch.int16), out.to(torch.bfloat16).view(torch.int16))
+            # refused with a relu output, on the VALU kernel and on other precisions
+            for bad in ((ptr(relu), XCORR_ALGOS["mfma"], pc), (None, XCORR_ALGOS["valu"], pc),
+                        (None, XCORR_ALGOS["mfma"], PREC_CODES["f16"])):
+                with pytest.raises(tmr_amd.TMRError):
+                    call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw,
+                         ptr(scale), 0, ptr(o16), bad[0], None, None, ptr(tsplit), rows, bad[1], 1, bad[2], 1,
+                         stream())
     tol = {"valu": TOL, "mfma": TOL if prec == "fp32" else XCORR_ONE_TERM_TOL[prec]}
     tmpl_h = tmpl.cpu().numpy()
     worst = 0.0
@@ -812,6 +833,33 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
             if pw:
                 assert (got[u][:, :, :pw] == 0).all() and (got[u][:, :, W - pw:] == 0).all()
     print(f"xcorr mfma {prec} {H}x{W}: worst normwise {worst:.3e}")
+
+
+def test_engine_bf16_ftm_plane_bitexact():
+    """Under the bf16 contract the detect path's correlation writes f_TM as
+    bf16 (tmr_xcorr_out) and the decoder packs it with tmr_split_xpack16: the
+    maps are bit-identical to the fp32-plane path (engine.out_bf16 = False),
+    for the shared (E = 3) and the unshared (E = 1) fp half."""
+    cin, emb, hf = 64, 128, 32
+    P = synth.reference_state_dict(9, cin=cin, emb=emb, obj_bias=-0.3)
+    for B, E in ((2, 3), (3, 1)):
+        feats = synth.sam_features(70 + E, B, cin, hf, hf)
+        ex, _ = synth.exemplar_set(71 + E, B, E, 2 * hf, 2 * hf, 3, 15)
+        ui = np.repeat(np.arange(B), E)
+        res = {}
+        for o16 in (False, True):
+            eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()},
+                                    tmr_amd.PathConfig(emb_dim=emb, precision="bf16"))
+            eng.xcorr_algo = "mfma"
+            eng.out_bf16 = o16
+            r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
+            assert eng.last_xcorr_out16 == o16
+            res[o16] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
+        for a, b in zip(res[False], res[True]):
+            assert bits_equal(a, b), (B, E)
+        # the module form (relu(f_TM) returned) keeps the fp32 plane
+        eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
+        assert not eng.last_xcorr_out16
 
 
 def test_xcorr_mfma_squeeze_and_engine():
