@@ -887,9 +887,14 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
 #define TMR_XPACK4_3T 0
 #endif
 constexpr int XSEG = TMR_XSEG;
+#ifndef TMR_XPACK16_RPB  // rows per block of the bf16-input record pack
+#define TMR_XPACK16_RPB 4
+#endif
 // IN: the activation's element type, float or __bf16 (a bf16 f_TM plane from
-// tmr_xcorr_out: bf16 records of it are its own elements, tmr_split_xpack16)
-template <int PREC, typename IN = float>
+// tmr_xcorr_out: bf16 records of it are its own elements, tmr_split_xpack16);
+// RPB rows of the segment per block (the bf16 form moves half the bytes per
+// row: 4 rows keep as many loads in flight per block).
+template <int PREC, typename IN = float, int RPB = 1>
 __global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, int S, int Cin, int H, int W,
                                                      int NCc, int Hp, int Wp, int pad, int64_t nseg,
                                                      int64_t nbord, const float *__restrict__ xmax,
@@ -898,46 +903,47 @@ __global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, i
     typedef typename Prec<PREC>::V V;
     typedef typename Prec<PREC>::E E;
     constexpr int VE = 16 / sizeof(IN);  // elements per 16-B load
+    constexpr int LPR = CCH * XSEG / VE;  // 16-B loads per row
     typedef IN INV __attribute__((ext_vector_type(VE)));
-    __shared__ __attribute__((aligned(16))) IN tile[CCH][XSEG];
+    __shared__ __attribute__((aligned(16))) IN tile[RPB][CCH][XSEG];
     const size_t plane = (size_t)Hp * Wp;
     const int t = threadIdx.x;
     if ((int64_t)blockIdx.x < nseg) {
-        const int nsx = (W + XSEG - 1) / XSEG;
+        const int nsx = (W + XSEG - 1) / XSEG, nyg = (H + RPB - 1) / RPB;
         int64_t r = blockIdx.x;
         const int sx = (int)(r % nsx);
         r /= nsx;
-        const int y = (int)(r % H);
-        r /= H;
+        const int y0 = (int)(r % nyg) * RPB;
+        r /= nyg;
         const int c = (int)(r % NCc);
         const int s = (int)(r / NCc);
         const int x0 = sx * XSEG, nx = min(XSEG, W - x0);  // nx % VE == 0
-        const IN *src = x + ((size_t)s * Cin + (size_t)c * CCH) * H * W + (size_t)y * W + x0;
+        const IN *src = x + ((size_t)s * Cin + (size_t)c * CCH) * H * W + (size_t)y0 * W + x0;
 #pragma unroll
-        for (int k = 0; k < CCH * XSEG / VE / 256; ++k) {
-            const int e = t + 256 * k, ch = e / (XSEG / VE), xv = e % (XSEG / VE);
+        for (int k = 0; k < RPB * LPR / 256; ++k) {
+            const int e = t + 256 * k, rr = e / LPR, ch = (e % LPR) / (XSEG / VE), xv = e % (XSEG / VE);
             INV v = {};
-            if (VE * xv < nx && c * CCH + ch < Cin)
-                v = *reinterpret_cast<const INV *>(src + (size_t)ch * H * W + VE * xv);
-            *reinterpret_cast<INV *>(&tile[ch][VE * xv]) = v;
+            if (VE * xv < nx && c * CCH + ch < Cin && y0 + rr < H)
+                v = *reinterpret_cast<const INV *>(src + (size_t)ch * H * W + (size_t)rr * W + VE * xv);
+            *reinterpret_cast<INV *>(&tile[rr][ch][VE * xv]) = v;
         }
         __syncthreads();
         const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
-        V *o = out + ((size_t)s * NCc + c) * HALVES * P * plane + (size_t)(y + pad) * Wp + x0 + pad;
+        V *o = out + ((size_t)s * NCc + c) * HALVES * P * plane + (size_t)(y0 + pad) * Wp + x0 + pad;
 #pragma unroll
-        for (int k = 0; k < XSEG * P / 256; ++k) {
-            const int e = t + 256 * k, q = e / XSEG, px = e % XSEG;
-            if (px < nx) {
+        for (int k = 0; k < RPB * XSEG * P / 256; ++k) {
+            const int e = t + 256 * k, rr = e / (XSEG * P), q = (e % (XSEG * P)) / XSEG, px = e % XSEG;
+            if (px < nx && y0 + rr < H) {
                 V hi, lo;
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {  // split_record's arithmetic
-                    const float xs = (float)tile[q * 8 + m][px] * sc;
+                    const float xs = (float)tile[rr][q * 8 + m][px] * sc;
                     const E h = (E)xs;
                     hi[m] = h;
                     if (HALVES == 2) lo[m] = (E)(xs - (float)h);
                 }
-                o[q * plane + px] = hi;
-                if (HALVES == 2) o[(P + q) * plane + px] = lo;
+                o[q * plane + (size_t)rr * Wp + px] = hi;
+                if (HALVES == 2) o[(P + q) * plane + (size_t)rr * Wp + px] = lo;
             }
         }
         return;
@@ -1163,10 +1169,12 @@ extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int 
                                  void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec == TMR_PREC_BF16);
     TMR_REQUIRE(W % 8 == 0);
+    constexpr int RPB = TMR_XPACK16_RPB;
     const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
-    const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
+    const int64_t nseg = (int64_t)S * NCc * tmr_cdiv(H, RPB) * tmr_cdiv(W, XSEG);
+    const int64_t nbord = (int64_t)Hp * Wp - (int64_t)H * W;
     const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
-    hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16, __bf16>), g4, dim3(256), 0, tmr_stream(stream),
+    hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16, __bf16, RPB>), g4, dim3(256), 0, tmr_stream(stream),
                        static_cast<const __bf16 *>(x), S, C, H, W, NCc, Hp, Wp, ks / 2, nseg, nbord, nullptr,
                        static_cast<b8 *>(out));
     TMR_CHECK_LAUNCH();
