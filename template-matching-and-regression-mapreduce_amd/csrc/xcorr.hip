@@ -523,6 +523,9 @@ constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
 #ifndef TMR_XCORR_PF1
 #define TMR_XCORR_PF1 4
 #endif
+#ifndef TMR_XCORR_PF3_WIDE  // 3-term kernel with >= 6 tiles per wave (W >= 192: LDS-bound occupancy)
+#define TMR_XCORR_PF3_WIDE 1
+#endif
 #ifndef TMR_XCORR_PF3
 #define TMR_XCORR_PF3 1
 #endif
@@ -678,7 +681,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int PF = SPLIT ? TMR_XCORR_PF3 : TMR_XCORR_PF1;  // prefetch distance (rows)
+    constexpr int PF = SPLIT ? (NTW >= 6 ? TMR_XCORR_PF3_WIDE : TMR_XCORR_PF3) : TMR_XCORR_PF1;  // (rows)
     V ah[PF][NK], al[PF][NK];
     auto afrag = [&](int i, int nk, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
