@@ -523,8 +523,8 @@ constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
 #ifndef TMR_XCORR_PF1
 #define TMR_XCORR_PF1 4
 #endif
-#ifndef TMR_XCORR_PF3_WIDE  // 3-term kernel with >= 6 tiles per wave (W >= 192: LDS-bound occupancy)
-#define TMR_XCORR_PF3_WIDE 1
+#ifndef TMR_XCORR_PF3_WIDE  // 3-term, >= 6 tiles per wave (W >= 192, LDS-bound occupancy): 3 rows (r03t)
+#define TMR_XCORR_PF3_WIDE 3
 #endif
 #ifndef TMR_XCORR_PF3
 #define TMR_XCORR_PF3 1
