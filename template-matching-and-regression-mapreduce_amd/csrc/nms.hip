@@ -232,10 +232,16 @@ __global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restr
     int cnt = s == 0 ? 0 : kept_out[g];
     __syncthreads();
     const int ib1 = (int)std::min<int64_t>(ib0 + S, nb);
+    // the row block's diagonal words do not depend on the chain: each is
+    // loaded one row block ahead, so its latency overlaps the previous
+    // block's OR loads instead of opening every block
+    uint64_t diag_next = (int)ib0 < ib1 && (int)ib0 * 64 + lane < n ? mask[(int64_t)lane * nb + ib0] : 0ull;
     for (int ib = (int)ib0; ib < ib1; ++ib) {
         const int i = ib * 64 + lane;
         const int64_t row = (int64_t)(ib - ib0) * 64;
-        const uint64_t diag = i < n ? mask[(row + lane) * nb + ib] : 0ull;
+        const uint64_t diag = diag_next;
+        if (ib + 1 < ib1)
+            diag_next = i + 64 < n ? mask[(row + 64 + lane) * nb + ib + 1] : 0ull;
         uint64_t word = removed[ib];
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
