@@ -59,3 +59,26 @@ __device__ __forceinline__ float up_value(const float *plane, int Hin, int Win, 
     float bot = fmaf(lx0, c, lx1 * d);
     return fmaf(ly0, top, ly1 * bot);
 }
+
+// Outputs (y, 4q .. 4q+3) of the same x2 upsample, bit-identical to four
+// up_value calls: away from the left/right edge the four columns read input
+// columns 2q-1 .. 2q+2 with the exact weights up_coord yields there
+// (x = 4q: 0.25/0.75, 4q+1: 0.75/0.25, 4q+2: 0.25/0.75, 4q+3: 0.75/0.25).
+__device__ __forceinline__ float4 up_value4(const float *plane, int Hin, int Win, int y, int q) {
+    if (q > 0 && 2 * q + 2 < Win) {
+        int y0, y1;
+        float ly0, ly1;
+        up_coord(y, Hin, y0, y1, ly0, ly1);
+        const float *r0 = plane + (size_t)y0 * Win + 2 * q - 1, *r1 = plane + (size_t)y1 * Win + 2 * q - 1;
+        const float a0 = r0[0], a1 = r0[1], a2 = r0[2], a3 = r0[3];
+        const float b0 = r1[0], b1 = r1[1], b2 = r1[2], b3 = r1[3];
+        const float t0 = fmaf(0.25f, a0, 0.75f * a1), u0 = fmaf(0.25f, b0, 0.75f * b1);
+        const float t1 = fmaf(0.75f, a1, 0.25f * a2), u1 = fmaf(0.75f, b1, 0.25f * b2);
+        const float t2 = fmaf(0.25f, a1, 0.75f * a2), u2 = fmaf(0.25f, b1, 0.75f * b2);
+        const float t3 = fmaf(0.75f, a2, 0.25f * a3), u3 = fmaf(0.75f, b2, 0.25f * b3);
+        return float4{fmaf(ly0, t0, ly1 * u0), fmaf(ly0, t1, ly1 * u1), fmaf(ly0, t2, ly1 * u2),
+                      fmaf(ly0, t3, ly1 * u3)};
+    }
+    return float4{up_value(plane, Hin, Win, y, 4 * q), up_value(plane, Hin, Win, y, 4 * q + 1),
+                  up_value(plane, Hin, Win, y, 4 * q + 2), up_value(plane, Hin, Win, y, 4 * q + 3)};
+}

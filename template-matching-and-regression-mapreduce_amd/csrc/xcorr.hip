@@ -49,6 +49,7 @@ struct XArgs {
     unsigned *out_absmax;  // nullable [TMR_ABSMAX_SLOTS]: slot-wise atomicMax of |out|
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
     int HG;                          // rows kernel: max template height / 2
+    int up;                          // f is the half-resolution plane [B][C][H/2][W/2]: stage up2x(f)
 };
 
 // x / d correctly rounded (= the reference's IEEE `/ (h*w + 1e-14)` in fp32)
@@ -420,7 +421,7 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     if (u_beg >= u_end) return;
     const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
     const int hg = a.HG;  // half of the largest template height: LDS row 0 = image row yb0 - hg
-    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * (a.up ? (H / 2) * (W / 2) : H * W);
     const float sc = a.squeeze ? 1.0f : *a.scale;  // read once, before any store
     // stage rows [yb0 - hg, yb0 - hg + LR) with zero pads (rows outside the image: zeros)
     // SU loads per thread in flight before any LDS write (a load -> ds_write
@@ -442,7 +443,8 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
             const int yy = yb0 - hg + lr;
             v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
             if (e < n4 && yy >= 0 && yy < H && cc >= 0 && cc < W4)
-                v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+                v[k] = a.up ? up_value4(fc, H / 2, W / 2, yy, cc)
+                            : reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
         }
 #pragma unroll
         for (int k = 0; k < SU; ++k)
@@ -605,7 +607,7 @@ __host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per templat
 
 __global__ __launch_bounds__(256) void template_split_kernel(const float *__restrict__ tmpl,
                                                              const tmr_unit_t *__restrict__ units, int U,
-                                                             int C, int64_t total_rows, int bf,
+                                                             int C, int64_t total_rows, int bf, int lo_too,
                                                              char *__restrict__ frags,
                                                              int32_t *__restrict__ exps) {
     // the wave's template through LDS (coalesced global reads once; the
@@ -646,15 +648,11 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 x[q] = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
             }
             char *f = dst + (size_t)((i * nk_u + nk) * 2) * AFRAG;
-            if (bf) {  // wave-uniform: bf16 hi / residual (the one-term bf16 MFMA reads hi only)
-                b8 hi, lo;
+            if (bf) {  // wave-uniform: bf16 hi (the one-term bf16 MFMA reads hi only)
+                b8 hi;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    hi[q] = (__bf16)x[q];
-                    lo[q] = (__bf16)(x[q] - (float)hi[q]);
-                }
+                for (int q = 0; q < 8; ++q) hi[q] = (__bf16)x[q];
                 *reinterpret_cast<b8 *>(f) = hi;
-                *reinterpret_cast<b8 *>(f + AFRAG) = lo;
             } else {
                 h8 hi, lo;
 #pragma unroll
@@ -663,7 +661,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                     lo[q] = (_Float16)(x[q] - (float)hi[q]);
                 }
                 *reinterpret_cast<h8 *>(f) = hi;
-                *reinterpret_cast<h8 *>(f + AFRAG) = lo;
+                if (lo_too) *reinterpret_cast<h8 *>(f + AFRAG) = lo;  // the 3-term kernel's tl
             }
         }
     if (lane == 0) exps[(int64_t)u * C + c] = et;
@@ -761,7 +759,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     float *red = reinterpret_cast<float *>(smem + NPL * (size_t)LR * SB);
     const int tid = threadIdx.x;
     const int yb0 = band * BR, yb1 = min(yb0 + BR, H);
-    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * (a.up ? (H / 2) * (W / 2) : H * W);
     const float sc = a.squeeze ? 1.0f : *a.scale;
 
     // ---- stage the band: fp32 -> registers -> block max -> fp16 hi/lo planes
@@ -775,7 +773,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
         const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
         const int yy = yb0 - hg + lr;
-        if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        if (e < n4 && yy >= 0 && yy < H)
+            v[k] = a.up ? up_value4(fc, H / 2, W / 2, yy, cc) : reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
         vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
     }
     // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
@@ -999,7 +998,7 @@ extern "C" int tmr_template_split_prec(const float *templates, const tmr_unit_t 
     const int64_t waves = (int64_t)U * C;
     hipLaunchKernelGGL(template_split_kernel, dim3((unsigned)tmr_cdiv(waves, 4)), dim3(256), 0,
                        tmr_stream(stream), templates, units, U, C, total_rows, (int)(prec == TMR_PREC_BF16),
-                       frags, ex);
+                       (int)(prec == TMR_PREC_F16X3), frags, ex);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
@@ -1014,8 +1013,11 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
                              int max_wt, const float *scale, int squeeze, void *out, float *relu_out,
                              float *work, float *out_absmax, const void *tmpl_split,
                              int64_t total_rows, int algo, int min_k, int prec, int out_bf16,
-                             void *stream) {
+                             int f_half, void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
+    // f_half: f is [B][C][H/2][W/2] and the kernels stage up2x(f) (bit-identical to
+    // tmr_upsample2x's plane); the MFMA and row-tiled kernels only, no squeeze
+    TMR_REQUIRE(!f_half || (H % 2 == 0 && W % 2 == 0 && !squeeze));
     // a bf16 f_TM plane: the one-term bf16 MFMA kernel only, no relu / squeeze outputs
     TMR_REQUIRE(!out_bf16 || (algo == TMR_XCORR_MFMA && prec == TMR_PREC_BF16 && !squeeze && !relu_out));
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
@@ -1036,6 +1038,7 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
     a.H = H;
     a.W = W;
     a.squeeze = squeeze;
+    a.up = f_half ? 1 : 0;
     hipStream_t s = tmr_stream(stream);
     TMR_REQUIRE(C < 65536 && B < 65536);
     const bool fits = mfma_fits(H, W, max_ht, max_wt) && tmpl_split && total_rows > 0;
@@ -1048,6 +1051,7 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
         // row-tiled kernel when rows are 16-B aligned and templates fit its
         // width specialisations (template sizes are odd, template_matching.py:66-73)
         const bool rows = (W % 4) == 0 && max_wt <= 31;
+        if (f_half && !rows) return TMR_E_UNSUPPORTED;  // the generic kernel reads a full-resolution f
         const int WS = rows ? W + PADL + PADR : W;
         // LDS rows: band + template halo + slack rows for partial 4-row tiles
         const int max_rows = (150 * 1024) / (4 * WS) - 1;
@@ -1089,7 +1093,7 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
                               float *work, float *out_absmax, const void *tmpl_split,
                               int64_t total_rows, int algo, int min_k, int prec, void *stream) {
     return tmr_xcorr_out(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
-                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, stream);
+                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, 0, stream);
 }
 
 extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
