@@ -767,15 +767,49 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     const float rw4 = 1.0f / (float)W4;  // e / W4 by one multiply (exact for e < 2^16)
     float4 v[NV4];
     float vm = 0.0f;
+    if (a.up) {
+        // fp = up2x(f) of the half-size plane: its input rows (all columns)
+        // staged in LDS by 16-B loads (in the planes' space, before they are
+        // written), then every thread forms its float4s from LDS
+        const int Hin = H / 2, Win = W / 2, Win4 = Win >> 2;
+        const int ylo = max(yb0 - hg, 0), yhi = min(yb0 - hg + LR, H) - 1;
+        int rlo, rhi, t0, t1;
+        float l0, l1;
+        up_coord(ylo, Hin, rlo, t0, l0, l1);
+        up_coord(yhi, Hin, t1, rhi, l0, l1);
+        float *win = reinterpret_cast<float *>(smem);
+        const int nw4 = (rhi - rlo + 1) * Win4;
+        const float rwin4 = 1.0f / (float)Win4;
+        for (int e = tid; e < nw4; e += NT) {
+            const int r = (int)(((float)e + 0.5f) * rwin4), cc = e - r * Win4;
+            reinterpret_cast<float4 *>(win)[e] = reinterpret_cast<const float4 *>(fc + (size_t)(rlo + r) * Win)[cc];
+        }
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NV4; ++k) {
-        const int e = tid + k * NT;
-        v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
-        const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
-        const int yy = yb0 - hg + lr;
-        if (e < n4 && yy >= 0 && yy < H)
-            v[k] = a.up ? up_value4(fc, H / 2, W / 2, yy, cc) : reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
-        vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
+        for (int k = 0; k < NV4; ++k) {
+            const int e = tid + k * NT;
+            v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+            const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
+            const int yy = yb0 - hg + lr;
+            if (e < n4 && yy >= 0 && yy < H) {
+                int y0, y1;
+                float ly0, ly1;
+                up_coord(yy, Hin, y0, y1, ly0, ly1);
+                v[k] = up_rows4(win + (y0 - rlo) * Win, win + (y1 - rlo) * Win, ly0, ly1, Win, cc);
+            }
+            vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
+        }
+        __syncthreads();  // the window's space is the planes'
+    } else {
+#pragma unroll
+        for (int k = 0; k < NV4; ++k) {
+            const int e = tid + k * NT;
+            v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+            const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
+            const int yy = yb0 - hg + lr;
+            if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+            vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
+        }
     }
     // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
     {

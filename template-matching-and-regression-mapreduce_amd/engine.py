@@ -413,6 +413,7 @@ class TMREngine:
         # detect path: fp stays at the SAM features' size and the template and
         # correlation kernels read its x2 upsample on the fly (HalfPlane)
         self.lazy_upsample = True
+        self.lazy_valu = False
         self.last_xcorr_f_half = False
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
@@ -685,8 +686,11 @@ class TMREngine:
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
-        if lazy and algo == XCORR_ALGOS["valu"] and not (W % 4 == 0 and mw <= 31):
-            fp, lazy = fp.full(), False  # the generic VALU kernel reads a full-resolution plane
+        if lazy and algo == XCORR_ALGOS["valu"] and not (self.lazy_valu and W % 4 == 0 and mw <= 31):
+            # the generic VALU kernel reads a full-resolution plane; the
+            # row-tiled one can read the half-size plane (tmr_xcorr_out f_half)
+            # but stays on the materialised plane unless lazy_valu is set
+            fp, lazy = fp.full(), False
         self.last_xcorr_f_half = lazy
         out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
                  and not cfg.squeeze and not want_relu and W % 8 == 0)

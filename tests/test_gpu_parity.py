@@ -932,7 +932,7 @@ def test_engine_half_plane_bitexact(prec):
         for lazy in (False, True):
             eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()},
                                     tmr_amd.PathConfig(emb_dim=emb, precision=prec))
-            eng.lazy_upsample = lazy
+            eng.lazy_upsample = eng.lazy_valu = lazy
             for algo in ("valu", "mfma"):
                 eng.xcorr_algo = algo
                 r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
