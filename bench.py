@@ -278,9 +278,6 @@ def main():
     eng.decoder_algo = a.decoder
     # A/B knob: TMR_BENCH_OUT_BF16=0 keeps the bf16 contract's f_TM plane in fp32
     eng.out_bf16 = os.environ.get("TMR_BENCH_OUT_BF16", "1") != "0"
-    # A/B knob: TMR_BENCH_LAZY_UP=0 materialises fp = up2x(projection) before the correlation
-    eng.lazy_upsample = os.environ.get("TMR_BENCH_LAZY_UP", "1") != "0"
-    eng.lazy_valu = os.environ.get("TMR_BENCH_LAZY_VALU", "0") != "0"
     B = a.batch or cfg["batch"]
     E = a.exemplars or cfg["E"]
     feats = synth.sam_features(1000 + rank, B, CIN, H // 2, W // 2)

@@ -95,13 +95,6 @@ int tmr_upsample2x(const float *feat, int BC, int Hin, int Win, float *out, void
  * (:52).  f [B,C,H,W]; templates written at units[u].tmpl_offset as [C,ht,wt]. */
 int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *units, int U,
                   int max_ht, int max_wt, float *templates, void *stream);
-/* The RoIAlign templates of up2x(f_half) without materialising it: f_half
- * [B,C,H/2,W/2] (H, W even) is the projection before the x2 upsample, and
- * every sample reads the upsampled value tmr_upsample2x would have stored
- * (same fma form): templates bit-identical to tmr_templates on that plane.
- * RoIAlign units only (prototype units are not written). */
-int tmr_templates_up(const float *f_half, int B, int C, int H, int W, const tmr_unit_t *units, int U,
-                     int max_ht, int max_wt, float *templates, void *stream);
 
 /* ---- (a9+a4) depthwise cross-correlation + pad + scale -------------------
  * out[u] = pad(conv2d(f[img(u)], T_u, groups=C) / fl32(ht*wt)) * scale
@@ -152,25 +145,19 @@ int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *temp
                    const float *scale, int squeeze, float *out, float *relu_out, float *work,
                    float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
                    int min_k, int prec, void *stream);
-/* tmr_xcorr_prec with the f_TM plane's element type and the input's
- * resolution chosen.  out_bf16 = 0 is tmr_xcorr_prec (out float
- * [U][C][H][W]); out_bf16 = 1 writes out as bf16 [U][C][H][W], each element
- * the round-to-nearest-even bf16 of the fp32 value tmr_xcorr_prec would
- * write -- the bf16 contract's detect path, whose decoder records
- * (tmr_split_xpack16) are those bf16 values.  out_bf16 needs algo
- * TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0 and relu_out NULL
- * (TMR_E_INVALID otherwise).  f_half = 1: f is [B][C][H/2][W/2] (H, W even),
- * the projection before the x2 upsample, and the kernels stage up2x(f) as
- * tmr_upsample2x would store it (bit-identical results, the full-resolution
- * plane never written); the MFMA and row-tiled kernels only (W % 4 == 0,
- * templates <= 31 wide: TMR_E_UNSUPPORTED otherwise), squeeze 0.  Same
- * sources as tmr_xcorr_prec: models/template_matching.py:23-41,97 and
- * matching_net.py:50-51,56. */
+/* tmr_xcorr_prec with the f_TM plane's element type chosen: out_bf16 = 0 is
+ * tmr_xcorr_prec (out float [U][C][H][W]); out_bf16 = 1 writes out as bf16
+ * [U][C][H][W], each element the round-to-nearest-even bf16 of the fp32
+ * value tmr_xcorr_prec would write -- the bf16 contract's detect path, whose
+ * decoder records (tmr_split_xpack16) are those bf16 values.  out_bf16 needs
+ * algo TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0 and relu_out NULL
+ * (TMR_E_INVALID otherwise).  Same sources as tmr_xcorr_prec:
+ * models/template_matching.py:23-41,97. */
 int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
                   const float *scale, int squeeze, void *out, float *relu_out, float *work,
                   float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
-                  int min_k, int prec, int out_bf16, int f_half, void *stream);
+                  int min_k, int prec, int out_bf16, void *stream);
 /* Operand prep of the MFMA correlation: per (unit u, channel c) template
  * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
  * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <

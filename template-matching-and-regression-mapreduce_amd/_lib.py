@@ -61,14 +61,13 @@ SIGNATURES = {
     "tmr_upsample_proj": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P]),
     "tmr_upsample2x": (_I, [_P, _I, _I, _I, _P, _P]),
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
-    "tmr_templates_up": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
     "tmr_xcorr_algo": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
                             _I, _I, _P]),
     "tmr_xcorr_prec": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
                             _I, _I, _I, _P]),
     "tmr_xcorr_out": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _L,
-                           _I, _I, _I, _I, _I, _P]),
+                           _I, _I, _I, _I, _P]),
     "tmr_template_split_size": (_L, [_I, _I, _L]),
     "tmr_template_split": (_I, [_P, _P, _I, _I, _L, _P, _P]),  # (..., total_rows, out, stream)
     "tmr_template_split_prec": (_I, [_P, _P, _I, _I, _L, _I, _P, _P]),  # (..., total_rows, prec, out, stream)

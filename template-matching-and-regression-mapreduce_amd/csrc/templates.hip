@@ -19,9 +19,6 @@ struct Samp {
     float w[4];
 };
 
-// UP: f is the half-resolution plane [B][C][H/2][W/2] and every sample reads
-// up2x(f) through up_value (bit-identical to tmr_upsample2x's plane)
-template <bool UP>
 __global__ __launch_bounds__(NT) void roi_align_kernel(const float *__restrict__ f, int C, int H,
                                                        int W, const tmr_unit_t *__restrict__ units,
                                                        float *__restrict__ tmpl) {
@@ -65,22 +62,20 @@ __global__ __launch_bounds__(NT) void roi_align_kernel(const float *__restrict__
         for (int k = threadIdx.x; k < ns; k += NT) samp[k] = make(k);
     __syncthreads();
 
-    const int Hq = UP ? H / 2 : H, Wq = UP ? W / 2 : W;
-    const float *fb = f + (size_t)un.image * C * Hq * Wq;
+    const float *fb = f + (size_t)un.image * C * H * W;
     float *out = tmpl + un.tmpl_offset;
     const int per_c = PH * PW;
-    auto fv = [&](const float *fc, int p) -> float { return UP ? up_value(fc, Hq, Wq, p / W, p % W) : fc[p]; };
     // this block's channel range (grid.y splits the unit's channels)
     const int c0 = (int)((int64_t)C * blockIdx.y / gridDim.y), c1 = (int)((int64_t)C * (blockIdx.y + 1) / gridDim.y);
     for (int e = c0 * per_c + threadIdx.x; e < c1 * per_c; e += NT) {
         const int c = e / per_c, q0 = (e % per_c) * g;
-        const float *fc = fb + (size_t)c * Hq * Wq;
+        const float *fc = fb + (size_t)c * H * W;
         float acc = 0.0f;
         for (int s = 0; s < g; ++s) {
             Samp sp = cached ? samp[q0 + s] : make(q0 + s);
-            float v = sp.w[0] * fv(fc, sp.p[0]) + sp.w[1] * fv(fc, sp.p[1]);
-            v = v + sp.w[2] * fv(fc, sp.p[2]);
-            v = v + sp.w[3] * fv(fc, sp.p[3]);
+            float v = sp.w[0] * fc[sp.p[0]] + sp.w[1] * fc[sp.p[1]];
+            v = v + sp.w[2] * fc[sp.p[2]];
+            v = v + sp.w[3] * fc[sp.p[3]];
             acc += v;
         }
         out[e] = acc / count;
@@ -116,21 +111,10 @@ extern "C" int tmr_templates(const float *f, int B, int C, int H, int W, const t
     // channel groups per unit: enough workgroups for the chip at small U
     // (the module API runs one unit per call), >= 8 channels each
     const int cg = (int)std::max<int64_t>(1, std::min<int64_t>(C / 8, tmr_cdiv(1024, U)));
-    hipLaunchKernelGGL(roi_align_kernel<false>, dim3(U, cg), dim3(NT), 0, s, f, C, H, W, units, templates);
+    hipLaunchKernelGGL(roi_align_kernel, dim3(U, cg), dim3(NT), 0, s, f, C, H, W, units, templates);
     TMR_CHECK_LAUNCH();
     hipLaunchKernelGGL(prototype_kernel, dim3(U, (unsigned)tmr_cdiv(C, NT / 64) > 64 ? 64 : (unsigned)tmr_cdiv(C, NT / 64)),
                        dim3(NT), 0, s, f, C, H, W, units, templates);
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
-}
-
-extern "C" int tmr_templates_up(const float *f_half, int B, int C, int H, int W, const tmr_unit_t *units,
-                                int U, int max_ht, int max_wt, float *templates, void *stream) {
-    TMR_REQUIRE(f_half && units && templates && B > 0 && C > 0 && H > 1 && W > 1 && U > 0);
-    TMR_REQUIRE(max_ht > 0 && max_wt > 0 && H % 2 == 0 && W % 2 == 0);
-    const int cg = (int)std::max<int64_t>(1, std::min<int64_t>(C / 8, tmr_cdiv(1024, U)));
-    hipLaunchKernelGGL(roi_align_kernel<true>, dim3(U, cg), dim3(NT), 0, tmr_stream(stream), f_half, C, H, W,
-                       units, templates);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

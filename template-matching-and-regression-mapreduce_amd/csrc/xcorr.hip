@@ -49,7 +49,6 @@ struct XArgs {
     unsigned *out_absmax;  // nullable [TMR_ABSMAX_SLOTS]: slot-wise atomicMax of |out|
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
     int HG;                          // rows kernel: max template height / 2
-    int up;                          // f is the half-resolution plane [B][C][H/2][W/2]: stage up2x(f)
 };
 
 // x / d correctly rounded (= the reference's IEEE `/ (h*w + 1e-14)` in fp32)
@@ -421,7 +420,7 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
     if (u_beg >= u_end) return;
     const int yb0 = band * a.RB, yb1 = min(yb0 + a.RB, H);
     const int hg = a.HG;  // half of the largest template height: LDS row 0 = image row yb0 - hg
-    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * (a.up ? (H / 2) * (W / 2) : H * W);
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
     const float sc = a.squeeze ? 1.0f : *a.scale;  // read once, before any store
     // stage rows [yb0 - hg, yb0 - hg + LR) with zero pads (rows outside the image: zeros)
     // SU loads per thread in flight before any LDS write (a load -> ds_write
@@ -443,8 +442,7 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
             const int yy = yb0 - hg + lr;
             v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
             if (e < n4 && yy >= 0 && yy < H && cc >= 0 && cc < W4)
-                v[k] = a.up ? up_value4(fc, H / 2, W / 2, yy, cc)
-                            : reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+                v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
         }
 #pragma unroll
         for (int k = 0; k < SU; ++k)
@@ -759,7 +757,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     float *red = reinterpret_cast<float *>(smem + NPL * (size_t)LR * SB);
     const int tid = threadIdx.x;
     const int yb0 = band * BR, yb1 = min(yb0 + BR, H);
-    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * (a.up ? (H / 2) * (W / 2) : H * W);
+    const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
     const float sc = a.squeeze ? 1.0f : *a.scale;
 
     // ---- stage the band: fp32 -> registers -> block max -> fp16 hi/lo planes
@@ -767,49 +765,14 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     const float rw4 = 1.0f / (float)W4;  // e / W4 by one multiply (exact for e < 2^16)
     float4 v[NV4];
     float vm = 0.0f;
-    if (a.up) {
-        // fp = up2x(f) of the half-size plane: its input rows (all columns)
-        // staged in LDS by 16-B loads (in the planes' space, before they are
-        // written), then every thread forms its float4s from LDS
-        const int Hin = H / 2, Win = W / 2, Win4 = Win >> 2;
-        const int ylo = max(yb0 - hg, 0), yhi = min(yb0 - hg + LR, H) - 1;
-        int rlo, rhi, t0, t1;
-        float l0, l1;
-        up_coord(ylo, Hin, rlo, t0, l0, l1);
-        up_coord(yhi, Hin, t1, rhi, l0, l1);
-        float *win = reinterpret_cast<float *>(smem);
-        const int nw4 = (rhi - rlo + 1) * Win4;
-        const float rwin4 = 1.0f / (float)Win4;
-        for (int e = tid; e < nw4; e += NT) {
-            const int r = (int)(((float)e + 0.5f) * rwin4), cc = e - r * Win4;
-            reinterpret_cast<float4 *>(win)[e] = reinterpret_cast<const float4 *>(fc + (size_t)(rlo + r) * Win)[cc];
-        }
-        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < NV4; ++k) {
-            const int e = tid + k * NT;
-            v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
-            const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
-            const int yy = yb0 - hg + lr;
-            if (e < n4 && yy >= 0 && yy < H) {
-                int y0, y1;
-                float ly0, ly1;
-                up_coord(yy, Hin, y0, y1, ly0, ly1);
-                v[k] = up_rows4(win + (y0 - rlo) * Win, win + (y1 - rlo) * Win, ly0, ly1, Win, cc);
-            }
-            vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
-        }
-        __syncthreads();  // the window's space is the planes'
-    } else {
-#pragma unroll
-        for (int k = 0; k < NV4; ++k) {
-            const int e = tid + k * NT;
-            v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
-            const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
-            const int yy = yb0 - hg + lr;
-            if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
-            vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
-        }
+    for (int k = 0; k < NV4; ++k) {
+        const int e = tid + k * NT;
+        v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
+        const int yy = yb0 - hg + lr;
+        if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
     }
     // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
     {
@@ -1047,11 +1010,8 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
                              int max_wt, const float *scale, int squeeze, void *out, float *relu_out,
                              float *work, float *out_absmax, const void *tmpl_split,
                              int64_t total_rows, int algo, int min_k, int prec, int out_bf16,
-                             int f_half, void *stream) {
+                             void *stream) {
     TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
-    // f_half: f is [B][C][H/2][W/2] and the kernels stage up2x(f) (bit-identical to
-    // tmr_upsample2x's plane); the MFMA and row-tiled kernels only, no squeeze
-    TMR_REQUIRE(!f_half || (H % 2 == 0 && W % 2 == 0 && !squeeze));
     // a bf16 f_TM plane: the one-term bf16 MFMA kernel only, no relu / squeeze outputs
     TMR_REQUIRE(!out_bf16 || (algo == TMR_XCORR_MFMA && prec == TMR_PREC_BF16 && !squeeze && !relu_out));
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
@@ -1072,7 +1032,6 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
     a.H = H;
     a.W = W;
     a.squeeze = squeeze;
-    a.up = f_half ? 1 : 0;
     hipStream_t s = tmr_stream(stream);
     TMR_REQUIRE(C < 65536 && B < 65536);
     const bool fits = mfma_fits(H, W, max_ht, max_wt) && tmpl_split && total_rows > 0;
@@ -1085,7 +1044,6 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
         // row-tiled kernel when rows are 16-B aligned and templates fit its
         // width specialisations (template sizes are odd, template_matching.py:66-73)
         const bool rows = (W % 4) == 0 && max_wt <= 31;
-        if (f_half && !rows) return TMR_E_UNSUPPORTED;  // the generic kernel reads a full-resolution f
         const int WS = rows ? W + PADL + PADR : W;
         // LDS rows: band + template halo + slack rows for partial 4-row tiles
         const int max_rows = (150 * 1024) / (4 * WS) - 1;
@@ -1127,7 +1085,7 @@ extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const 
                               float *work, float *out_absmax, const void *tmpl_split,
                               int64_t total_rows, int algo, int min_k, int prec, void *stream) {
     return tmr_xcorr_out(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
-                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, 0, stream);
+                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, stream);
 }
 
 extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,

@@ -354,26 +354,6 @@ def _units_to_device(units: np.ndarray, device) -> torch.Tensor:
     return _h2d(units.view(np.uint8), device)
 
 
-class HalfPlane:
-    """fp = up2x(half) left unmaterialised: the projection at the SAM
-    features' size, read through the x2 upsample on the fly by the template
-    and correlation kernels (tmr_templates_up, tmr_xcorr_out f_half), whose
-    results are bit-identical to those on the materialised plane; full()
-    materialises it (tmr_upsample2x) for any other consumer."""
-
-    def __init__(self, half: torch.Tensor):
-        self.half = half
-        B, C, h, w = half.shape
-        self.shape = (B, C, 2 * h, 2 * w)
-        self.device = half.device
-
-    def full(self) -> torch.Tensor:
-        B, C, H, W = self.shape
-        fp = torch.empty(self.shape, device=self.device, dtype=torch.float32)
-        call("tmr_upsample2x", ptr(self.half), B * C, H // 2, W // 2, ptr(fp), stream())
-        return fp
-
-
 class TMREngine:
     """Native forward + post-processing over (image, exemplar) units."""
 
@@ -410,11 +390,6 @@ class TMREngine:
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
         self.last_xcorr_out16 = False
-        # detect path: fp stays at the SAM features' size and the template and
-        # correlation kernels read its x2 upsample on the fly (HalfPlane)
-        self.lazy_upsample = True
-        self.lazy_valu = False
-        self.last_xcorr_f_half = False
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
@@ -573,10 +548,8 @@ class TMREngine:
         self._absmax_memo[key] = (weakref.ref(t), t._version, val)
         return val
 
-    def project(self, feats: torch.Tensor, want_f0: bool = False, lazy: bool = False):
-        """fp = input_proj(up2x(feats)) [B,emb,H,W] (+ f0 = up2x(feats)); with
-        lazy, fp may come back as a HalfPlane (the projection before the x2
-        upsample, for consumers that read up2x on the fly)."""
+    def project(self, feats: torch.Tensor, want_f0: bool = False):
+        """fp = input_proj(up2x(feats)) [B,emb,H,W] (+ f0 = up2x(feats))."""
         require_gpu(feats, "features")
         feats = feats.float().contiguous()
         B, Cin, Hin, Win = feats.shape
@@ -615,9 +588,7 @@ class TMREngine:
             call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
                  ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
                  0, stream())
-            if early and lazy:
-                fp = HalfPlane(fq)
-            elif early:
+            if early:
                 fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
                 call("tmr_upsample2x", ptr(fq), B * N, Hin, Win, ptr(fp), stream())
             else:
@@ -646,26 +617,17 @@ class TMREngine:
         """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu).
         allow_bf16: the caller only packs f_TM into bf16 decoder records (the
         bf16 contract's detect path), so the one-term bf16 MFMA kernel may
-        write it as bf16 (tmr_xcorr_out; the records are bit-identical).
-        fp may be a HalfPlane (project(lazy=True)): RoIAlign templates and the
-        MFMA / row-tiled correlation then read up2x of the half-size plane on
-        the fly; any other path materialises it first."""
+        write it as bf16 (tmr_xcorr_out; the records are bit-identical)."""
         B, C, H, W = fp.shape
         U = len(unit_image)
         cfg = self.cfg
-        lazy = isinstance(fp, HalfPlane)
-        if lazy and (cfg.template_type != "roi_align" or cfg.squeeze):
-            fp, lazy = fp.full(), False
         units, tfl, mh, mw = host.build_units(unit_boxes, unit_image, H, W, C, cfg.template_type)
         dev = fp.device
         units_d = _units_to_device(units, dev)
         img_units = host.image_ranges(unit_image, B)  # units are sorted by image
         img_units_d = _h2d(np.asarray(img_units), dev)
         tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
-        if lazy:
-            call("tmr_templates_up", ptr(fp.half), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
-        else:
-            call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
+        call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
         Co = 1 if cfg.squeeze else C
         work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
         scale = self.P["matcher.scale"].detach().float().contiguous()
@@ -686,12 +648,6 @@ class TMREngine:
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
-        if lazy and algo == XCORR_ALGOS["valu"] and not (self.lazy_valu and W % 4 == 0 and mw <= 31):
-            # the generic VALU kernel reads a full-resolution plane; the
-            # row-tiled one can read the half-size plane (tmr_xcorr_out f_half)
-            # but stays on the materialised plane unless lazy_valu is set
-            fp, lazy = fp.full(), False
-        self.last_xcorr_f_half = lazy
         out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
                  and not cfg.squeeze and not want_relu and W % 8 == 0)
         self.last_xcorr_out16 = out16
@@ -703,11 +659,10 @@ class TMREngine:
             rows = host.tsplit_rows(units)
             tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
             call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
-        call("tmr_xcorr_out", ptr(fp.half if lazy else fp), B, C, H, W, ptr(tmpl), ptr(units_d),
-             ptr(img_units_d), U, mh, mw, ptr(scale), int(cfg.squeeze), ptr(out),
-             ptr(relu) if relu is not None else None, ptr(work) if work is not None else None, ptr(slots),
-             ptr(tsplit) if tsplit is not None else None, rows if tsplit is not None else 0, algo, min_k, pc,
-             int(out16), int(lazy), stream())
+        call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+             mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
+             ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
+             rows if tsplit is not None else 0, algo, min_k, pc, int(out16), stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
@@ -717,11 +672,9 @@ class TMREngine:
         self.last_xcorr_flops = float(np.sum(2.0 * C * (H - ht + 1) * (W - wt + 1) * ht * wt))
         self.last_xcorr_bytes = 2.0 * 4 * C * H * W * U
         # the minimum DRAM traffic of this launch: the kernels stage each
-        # image's fp plane once for all its units (read once per IMAGE; a
-        # quarter of it when they read the half-size plane), and write one
-        # f_TM plane per unit (half the bytes when it is bf16)
-        n_img = len(set(int(i) for i in unit_image))
-        self.last_xcorr_dram_bytes = 4.0 * C * H * W * (n_img * (0.25 if lazy else 1.0) + U * (0.5 if out16 else 1.0))
+        # image's fp plane once for all its units (read once per IMAGE), and
+        # write one f_TM plane per unit
+        self.last_xcorr_dram_bytes = 4.0 * C * H * W * (len(set(int(i) for i in unit_image)) + U)
         self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 
@@ -730,14 +683,11 @@ class TMREngine:
         """Decoders + heads over cat([fp[img(u)], f_TM[u]]) -> o [U,1,H,W], b [U,4,H,W]|None.
         feats (the SAM features fp was projected from) enables the folded fp half."""
         cfg = self.cfg
-        if isinstance(fp, HalfPlane) and not (cfg.decoder_num_layer == 1 and self.decoder_algo == "split"
-                                              and cfg.fusion and self.fold_proj and feats is not None):
-            fp = fp.full()  # only the folded fp half never reads fp
         U, C1, H, W = f_tm.shape
         dev = f_tm.device
         C0 = fp.shape[1] if cfg.fusion else 0
         ui = _h2d(np.asarray(unit_image, np.int32), dev)
-        src0 = fp if cfg.fusion and isinstance(fp, torch.Tensor) else None
+        src0 = fp if cfg.fusion else None
         if cfg.decoder_num_layer == 1:
             B = fp.shape[0]
             # share the fp half of the decoder conv across an image's exemplars
@@ -925,13 +875,7 @@ class TMREngine:
                     call("tmr_upsample2x", ptr(feats.float().contiguous()), B * Cin, Hin, Win, ptr(f0),
                          stream())
         else:
-            # the detect path's fp feeds only the templates, the correlation
-            # and the folded decoder: leave it at the features' size
-            cfg = self.cfg
-            lazy = (self.lazy_upsample and not want_aux and not self.reuse_image_work and not cfg.no_matcher
-                    and self.decoder_algo == "split" and cfg.decoder_num_layer == 1 and self.fold_proj
-                    and cfg.template_type == "roi_align" and not cfg.squeeze)
-            fp, f0 = self.project(feats, want_f0=want_aux, lazy=lazy)
+            fp, f0 = self.project(feats, want_f0=want_aux)
             if self.reuse_image_work:
                 self._fp_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), pkey, fp,
                                  tuple(weakref.ref(t) for t in params))

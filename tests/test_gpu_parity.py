@@ -805,7 +805,7 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
             # tmr_xcorr_out's bf16 plane: RNE bf16 of the fp32 plane, bit for bit
             o16 = torch.empty((U, C, H, W), device=DEV, dtype=torch.bfloat16)
             call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
-                 ptr(o16), None, None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, 1, 0, stream())
+                 ptr(o16), None, None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, 1, stream())
             torch.cuda.synchronize()
             assert torch.equal(o16.view(torch.int16), out.to(torch.bfloat16).view(torch.int16))
             # refused with a relu output, on the VALU kernel and on other precisions
@@ -814,7 +814,7 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
                 with pytest.raises(tmr_amd.TMRError):
                     call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw,
                          ptr(scale), 0, ptr(o16), bad[0], None, None, ptr(tsplit), rows, bad[1], 1, bad[2], 1,
-                         0, stream())
+                         stream())
     tol = {"valu": TOL, "mfma": TOL if prec == "fp32" else XCORR_ONE_TERM_TOL[prec]}
     tmpl_h = tmpl.cpu().numpy()
     worst = 0.0
@@ -860,89 +860,6 @@ def test_engine_bf16_ftm_plane_bitexact():
         # the module form (relu(f_TM) returned) keeps the fp32 plane
         eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
         assert not eng.last_xcorr_out16
-
-
-@pytest.mark.parametrize("H,W,prec", [(128, 128, "fp32"), (64, 96, "bf16"), (192, 192, "fp32"), (32, 40, "fp32")])
-def test_half_plane_templates_and_xcorr_bitexact(H, W, prec):
-    """fp left at the features' size (engine.HalfPlane): tmr_templates_up and
-    tmr_xcorr_out(f_half=1) read up2x of the half-size plane on the fly and
-    must equal tmr_templates / tmr_xcorr_out on the materialised
-    tmr_upsample2x plane bit for bit (edge columns and rows included), on the
-    MFMA and the row-tiled VALU kernel; the generic VALU kernel refuses it."""
-    from tmr_amd._lib import PREC_CODES, XCORR_ALGOS, call, ptr, stream
-    from tmr_amd.engine import _h2d, _units_to_device
-    B, C = 2, 16
-    half = cuda(synth.normal(77 + H + W, (B, C, H // 2, W // 2)) * 1.3)
-    full = torch.empty((B, C, H, W), device=DEV)
-    call("tmr_upsample2x", ptr(half), B * C, H // 2, W // 2, ptr(full), stream())
-    shapes = [(3, 3), (5, 9), (7, 7), (15, 15), (11, 3), (31, 31), (1, 1), (9, 1), (13, 21)]
-    shapes = [(min(kh, H // 2 * 2 - 1), min(kw, W // 2 * 2 - 1)) for kh, kw in shapes]
-    boxes, ui = [], []
-    for u, (kh, kw) in enumerate(shapes):  # corners and edges included
-        y0 = [0, H - kh, (5 * u) % (H - kh + 1)][u % 3]
-        x0 = [W - kw, 0, (7 * u) % (W - kw + 1)][u % 3]
-        boxes.append(synth.exemplar_box(kh, H, W, y0, x0, kw))
-        ui.append(u * B // len(shapes))
-    units, tfl, mh, mw = host.build_units(np.stack(boxes), ui, H, W, C)
-    ud = _units_to_device(units, DEV)
-    iu = _h2d(host.image_ranges(ui, B), DEV)
-    U = len(ui)
-    t_full = torch.empty(tfl, device=DEV)
-    t_up = torch.full((tfl,), float("nan"), device=DEV)
-    call("tmr_templates", ptr(full), B, C, H, W, ptr(ud), U, mh, mw, ptr(t_full), stream())
-    call("tmr_templates_up", ptr(half), B, C, H, W, ptr(ud), U, mh, mw, ptr(t_up), stream())
-    assert torch.equal(t_full.view(torch.int32), t_up.view(torch.int32))
-    pc = PREC_CODES[prec]
-    rows = host.tsplit_rows(units)
-    tsplit = torch.empty(tmr_amd._lib.load().tmr_template_split_size(U, C, rows), device=DEV, dtype=torch.uint8)
-    call("tmr_template_split_prec", ptr(t_full), ptr(ud), U, C, rows, pc, ptr(tsplit), stream())
-    scale = torch.tensor([0.75], device=DEV)
-    for algo in ("valu", "mfma"):
-        if algo == "mfma" and W % 32:
-            continue
-        outs = []
-        for fh, src in ((0, full), (1, half)):
-            out = torch.full((U, C, H, W), float("nan"), device=DEV)
-            amax = torch.zeros(256, device=DEV)
-            call("tmr_xcorr_out", ptr(src), B, C, H, W, ptr(t_full), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
-                 ptr(out), None, None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, 0, fh, stream())
-            outs.append(out)
-        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), algo
-    # the generic VALU kernel (W % 4 != 0) reads a full-resolution plane only
-    Wg = W - 2 if W % 4 == 0 else W
-    with pytest.raises(tmr_amd.TMRError):
-        call("tmr_xcorr_out", ptr(half), B, C, H, Wg, ptr(t_full), ptr(ud), ptr(iu), U, min(mh, 3), 3,
-             ptr(scale), 0, ptr(torch.empty((U, C, H, Wg), device=DEV)), None, None, None, None, 0,
-             XCORR_ALGOS["valu"], 1, pc, 0, 1, stream())
-
-
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_engine_half_plane_bitexact(prec):
-    """TMREngine with fp left at the features' size (lazy_upsample, the
-    detect path) against the materialised plane: o / b bit-identical, for the
-    shared (E = 3) and the unshared (E = 1) fp half; the module form (relu
-    and f[0] outputs) keeps the materialised plane."""
-    cin, emb, hf = 64, 128, 32
-    P = synth.reference_state_dict(12, cin=cin, emb=emb, obj_bias=-0.3)
-    for B, E in ((2, 3), (3, 1)):
-        feats = synth.sam_features(80 + E, B, cin, hf, hf)
-        ex, _ = synth.exemplar_set(81 + E, B, E, 2 * hf, 2 * hf, 1, 31)
-        ui = np.repeat(np.arange(B), E)
-        res = {}
-        for lazy in (False, True):
-            eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()},
-                                    tmr_amd.PathConfig(emb_dim=emb, precision=prec))
-            eng.lazy_upsample = eng.lazy_valu = lazy
-            for algo in ("valu", "mfma"):
-                eng.xcorr_algo = algo
-                r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
-                assert eng.last_xcorr_f_half == lazy, (lazy, algo)
-                res[(lazy, algo)] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
-        for algo in ("valu", "mfma"):
-            for a, b in zip(res[(False, algo)], res[(True, algo)]):
-                assert bits_equal(a, b), (prec, B, E, algo)
-        eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
-        assert not eng.last_xcorr_f_half
 
 
 def test_xcorr_mfma_squeeze_and_engine():
