@@ -1,15 +1,17 @@
-"""Randomised parity sweep: 24 seeded configurations of the detect path away
+"""Randomised parity sweep: 64 seeded configurations of the detect path away
 from the graded shapes -- rectangular and non-multiple-of-32 maps (the generic
 and row-tiled VALU correlation kernels, band edges, padded decoder tiles),
 1..4 images x 1..5 exemplars (shared and unshared fp half), template sides
 1..31 up to the map size, small and odd channel counts, random objectness
-bias, scale and thresholds -- each against the oracle exactly as the headline
-tests check the graded batches:
+bias, scale and thresholds, and the three precision contracts -- each against
+the oracle exactly as the headline tests check the graded batches:
 
-* maps o, b within 1e-5 normwise of oracle.forward_torch;
+* maps o, b within the contract's normwise tolerance of oracle.forward_torch
+  (fp32 1e-5, f16 1e-3, bf16 1e-2: SURVEY.md §8d);
 * TMREngine.detect's kept logits / boxes / refs bit-exact to the oracle's
   peaks + NMS on the GPU's own maps (demo.py:111-130 sequence);
-* the agreement contract against the oracle's own maps (oracle/agreement.py).
+* on the fp32 contract, the agreement contract against the oracle's own maps
+  (oracle/agreement.py).
 
 The configurations are drawn from a fixed seed, so the sweep is the same on
 every run; each one takes about a second of CPU oracle.
@@ -25,7 +27,7 @@ from tmr_amd import synth
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1e-5
+TOL = {"fp32": 1e-5, "f16": 1e-3, "bf16": 1e-2}
 DEV = torch.device("cuda:0")
 
 
@@ -56,10 +58,11 @@ def draw(seed):
     kmin = min(kmin, kmax)
     return dict(hf=hf, wf=wf, cin=cin, emb=emb, B=B, E=E, kmin=kmin, kmax=kmax,
                 bias=float(r.uniform(-0.6, 0.6)), scale=float(r.uniform(0.3, 2.0)),
-                cls=float(r.choice([0.05, 0.1, 0.3, 0.5])), iou=float(r.choice([0.3, 0.5, 0.7])))
+                cls=float(r.choice([0.05, 0.1, 0.3, 0.5])), iou=float(r.choice([0.3, 0.5, 0.7])),
+                precision=str(r.choice(["fp32", "fp32", "fp32", "bf16", "f16"])) if seed >= 24 else "fp32")
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(64))
 def test_random_config_vs_oracle(seed):
     c = draw(seed)
     P = synth.reference_state_dict(300 + seed, cin=c["cin"], emb=c["emb"], obj_bias=c["bias"])
@@ -68,7 +71,9 @@ def test_random_config_vs_oracle(seed):
     H, W = 2 * c["hf"], 2 * c["wf"]
     ex, _ = synth.exemplar_set(500 + seed, c["B"], c["E"], H, W, c["kmin"], c["kmax"])
     B, E = c["B"], c["E"]
-    eng = tmr_amd.TMREngine({k: v.to(DEV) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=c["emb"]))
+    prec = c["precision"]
+    eng = tmr_amd.TMREngine({k: v.to(DEV) for k, v in P.items()},
+                            tmr_amd.PathConfig(emb_dim=c["emb"], precision=prec))
     fd = torch.from_numpy(feats).to(DEV)
     L, Bx, R = eng.detect(fd, ex, cls_ths=c["cls"], iou_threshold=c["iou"])
     ui = np.repeat(np.arange(B), E)
@@ -84,7 +89,7 @@ def test_random_config_vs_oracle(seed):
             ro, rb = ro[0][0].numpy(), rb[0][0].numpy()
             eo, eb = normwise(o[u], ro), normwise(b[u], rb)
             worst = max(worst, eo, eb)
-            assert eo <= TOL and eb <= TOL, (c, img, e, eo, eb)
+            assert eo <= TOL[prec] and eb <= TOL[prec], (c, img, e, eo, eb)
             omaps.append((oracle.sigmoid_cr(ro[0]), rb))
         gmaps = agreement.unit_maps(o[units], b[units])
         ls, bs, rs = [], [], []
@@ -96,6 +101,7 @@ def test_random_config_vs_oracle(seed):
         assert bits_equal(L[img].cpu().numpy(), gl[0]), (c, img)
         assert bits_equal(Bx[img].cpu().numpy(), gb[0]), (c, img)
         assert bits_equal(R[img].cpu().numpy(), gr[0]), (c, img)
-        agreement.check(agreement.compare(omaps, gmaps, list(ex[img]), c["cls"], c["iou"]))
+        if prec == "fp32":
+            agreement.check(agreement.compare(omaps, gmaps, list(ex[img]), c["cls"], c["iou"]))
     print(f"seed {seed}: {c} xcorr={eng.last_xcorr_algo} kept={[int(x.shape[0]) for x in L]} "
           f"worst normwise {worst:.2e}")
