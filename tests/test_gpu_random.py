@@ -14,7 +14,7 @@ the oracle exactly as the headline tests check the graded batches:
   (oracle/agreement.py).
 
 The configurations are drawn from a fixed seed, so the sweep is the same on
-every run; each one takes about a second of CPU oracle.
+every run; the 64 take a few seconds of CPU oracle.
 """
 import numpy as np
 import pytest
