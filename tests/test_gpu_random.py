@@ -105,3 +105,70 @@ def test_random_config_vs_oracle(seed):
             agreement.check(agreement.compare(omaps, gmaps, list(ex[img]), c["cls"], c["iou"]))
     print(f"seed {seed}: {c} xcorr={eng.last_xcorr_algo} kept={[int(x.shape[0]) for x in L]} "
           f"worst normwise {worst:.2e}")
+
+
+class _Passthrough(torch.nn.Module):
+    """The `features` backbone: the module input is the SAM feature map."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.num_channels = c
+
+    def forward(self, x):
+        return x
+
+
+def draw_variant(seed):
+    """A module configuration: the reference's architecture switches
+    (models/matching_net.py:18-42, template_matching.py:15-21) and shapes."""
+    r = np.random.default_rng(5678 + seed)
+    no_matcher = bool(r.random() < 0.1)
+    return dict(
+        hf=int(r.choice([8, 12, 16, 20])), wf=int(r.choice([8, 12, 16, 20])), cin=int(r.choice([8, 16, 24])),
+        emb=int(r.choice([8, 16, 24])), B=int(r.integers(1, 4)),
+        squeeze=bool(r.random() < 0.2) and not no_matcher,
+        template_type="prototype" if r.random() < 0.2 else "roi_align",
+        fusion=bool(r.random() >= 0.15), box_reg=bool(r.random() >= 0.15),
+        layers=int(r.choice([1, 1, 1, 2])), k=int(r.choice([3, 3, 3, 5, 1])),
+        upsample=bool(r.random() >= 0.15), no_matcher=no_matcher,
+        bias=float(r.uniform(-0.5, 0.5)), scale=float(r.uniform(0.5, 1.5)))
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_module_variant_vs_oracle(seed):
+    """matching_net built from the reference's args (every architecture
+    switch drawn at random) called in the reference's module form, against
+    oracle.forward_torch with the same switches: o, b, relu(f_TM) within 1e-5
+    normwise, f[0] within 1e-6 (its fma form is bit-exact with the C oracle)."""
+    from types import SimpleNamespace
+    c = draw_variant(seed)
+    args = SimpleNamespace(emb_dim=c["emb"], fusion=c["fusion"], ablation_no_box_regression=not c["box_reg"],
+                           encoder="original", feature_upsample=c["upsample"], no_matcher=c["no_matcher"],
+                           template_type=c["template_type"], squeeze=c["squeeze"],
+                           decoder_num_layer=c["layers"], decoder_kernel_size=c["k"], modeltype="matching_net")
+    P = oracle.reference_weights(700 + seed, cin=c["cin"], emb=c["emb"], num_layers=c["layers"], k=c["k"],
+                                 squeeze=c["squeeze"], fusion=c["fusion"], box_reg=c["box_reg"])
+    P["objectness_head.head.0.bias"] = torch.tensor([c["bias"]])
+    P["matcher.scale"] = torch.tensor([c["scale"]])
+    if c["no_matcher"]:
+        del P["matcher.scale"]
+    model = tmr_amd.matching_net(_Passthrough(c["cin"]), args)
+    model.load_state_dict(P, strict=True)
+    model = model.to(DEV).eval()
+    feats = synth.sam_features(800 + seed, c["B"], c["cin"], c["hf"], c["wf"])
+    H, W = (2 * c["hf"], 2 * c["wf"]) if c["upsample"] else (c["hf"], c["wf"])
+    ex, _ = synth.exemplar_set(900 + seed, c["B"], 1, H, W, 1, min(9, 2 * (min(H, W) // 4) + 1))
+    with torch.no_grad():
+        os_, bs_, ftm, f0 = model(torch.from_numpy(feats).to(DEV), [torch.from_numpy(e).to(DEV) for e in ex])
+    ro, rb, rf, r0 = oracle.forward_torch(torch.from_numpy(feats), [torch.from_numpy(e) for e in ex], P,
+                                          feature_upsample=c["upsample"], fusion=c["fusion"],
+                                          squeeze=c["squeeze"], box_reg=c["box_reg"],
+                                          template_type=c["template_type"], no_matcher=c["no_matcher"])
+    errs = [normwise(os_[0].cpu().numpy(), ro[0].numpy()), normwise(ftm[0].cpu().numpy(), rf[0].numpy())]
+    if c["box_reg"]:
+        errs.append(normwise(bs_[0].cpu().numpy(), rb[0].numpy()))
+    else:
+        assert bs_[0] is None
+    assert max(errs) <= 1e-5, (c, errs)
+    assert normwise(f0.cpu().numpy(), r0.numpy()) <= 1e-6, c
+    print(f"variant seed {seed}: {c} worst normwise {max(errs):.2e}")
