@@ -952,13 +952,8 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
                        const void *tmpl_split, int64_t total_rows, int prec, bool out16) {
     MArgs m;
     // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
-    // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*); 16-row
-    // bands from TMR_XCORR_TRB1_MINW columns up under the 3-term split
-    // (experiment knob, 0 = never)
-#ifndef TMR_XCORR_TRB1_MINW
-#define TMR_XCORR_TRB1_MINW 0
-#endif
-    const int trb = TMR_XCORR_TRB1_MINW > 0 && a.W >= TMR_XCORR_TRB1_MINW && prec == TMR_PREC_F16X3 && !out16 ? 1 : 2;
+    // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*)
+    const int trb = 2;
     m.HG = max_ht / 2;
     m.HTM = max_ht;
     m.LR = 16 * trb + 2 * m.HG;
@@ -979,9 +974,7 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
         return prec == TMR_PREC_BF16 ? launch_mfma_w<2, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp, nv4)
                                      : TMR_E_UNSUPPORTED;
     switch (prec) {
-        case TMR_PREC_F16X3:
-            return trb == 1 ? launch_mfma_w<1, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4)
-                            : launch_mfma_w<2, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_F16X3: return launch_mfma_w<2, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
         case TMR_PREC_BF16: return launch_mfma_w<2, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
         case TMR_PREC_F16: return launch_mfma_w<2, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp, nv4);
         default: return TMR_E_INVALID;
