@@ -905,6 +905,7 @@ __global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, i
     constexpr int VE = 16 / sizeof(IN);  // elements per 16-B load
     constexpr int LPR = CCH * XSEG / VE;  // 16-B loads per row
     typedef IN INV __attribute__((ext_vector_type(VE)));
+    static_assert(RPB * LPR % 256 == 0 && RPB * XSEG * P % 256 == 0 && XSEG % VE == 0, "xpack4 tiling");
     __shared__ __attribute__((aligned(16))) IN tile[RPB][CCH][XSEG];
     const size_t plane = (size_t)Hp * Wp;
     const int t = threadIdx.x;
