@@ -360,6 +360,20 @@ int tmr_nms(const float *logits, const float *box, const float *ref, const int32
 int64_t tmr_feature_stats_work_size(int B);
 int tmr_feature_stats(const float *x, int B, int64_t n, void *work, double *out, void *stream);
 
+/* ---- the decode's reference-exp table, compact form ------------------------
+ * Host-only (no device pointers, no stream).  The table of fp32 inputs where
+ * the reference's torch.exp (utils/TM_utils.py:272, MKL vsExp on the golden
+ * host) is not the correctly rounded exp (tmr_amd/exp_table.py) is committed
+ * as a range-coded candidate bitmap (csrc/exp_codec.cpp).
+ * tmr_exp_table_encode: `exc` = the n recorded fp32 bit patterns, sorted
+ * (positive x first); out = NULL returns the blob size; else writes it and
+ * returns its size (< 0: TMR_E_INVALID, or TMR_E_UNSUPPORTED when an input
+ * lies outside the codec's candidate set).
+ * tmr_exp_table_decode: out = NULL returns the recorded count; else writes
+ * the sorted bit patterns and returns the count (< 0 on a malformed blob). */
+int64_t tmr_exp_table_encode(const uint32_t *exc, int64_t n, uint8_t *out, int64_t cap);
+int64_t tmr_exp_table_decode(const uint8_t *blob, int64_t nbytes, uint32_t *out, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,6 +98,8 @@ SIGNATURES = {
     "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),
     "tmr_feature_stats_work_size": (_L, [_I]),
     "tmr_feature_stats": (_I, [_P, _I, _L, _P, _P, _P]),
+    "tmr_exp_table_encode": (_L, [_P, _L, _P, _L]),
+    "tmr_exp_table_decode": (_L, [_P, _L, _P, _L]),
 }
 
 

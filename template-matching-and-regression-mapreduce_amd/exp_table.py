@@ -24,17 +24,22 @@ own golden outputs (tests/golden/pred_boxes.npz, caller.npz).
 
 Table file (little endian): 128-byte header (magic, count, domain, torch
 version, host CPU model), uint32 offsets[65537] indexed by the input's upper
-16 bits, then the sorted lower 16 bits of every recorded input (uint16).  Generated by
-``__graft_entry__.build()`` into the package directory (git-ignored, like
-libtmr.so; it travels with the tree).
+16 bits, then the sorted lower 16 bits of every recorded input (uint16).  It
+is expanded by ``__graft_entry__.build()`` into the package directory
+(git-ignored, like libtmr.so) from the COMMITTED compact form ``exp_ref.rc``
+(1.3 MB): a range-coded bitmap over the inputs near a rounding midpoint
+(csrc/exp_codec.cpp, ``tmr_exp_table_decode``), so a clean checkout builds the
+table on any x86-64 host, whatever its own torch.exp does.
 
 Pinning.  The table is the golden host's (GOLDEN_CPU, the host that wrote
-tests/golden/*), and its SHA-256 is GOLDEN_SHA256.  ``exp_sample.npz``
-(committed) holds 16384 inputs -- half of them recorded exceptions -- with
-the golden host's torch.exp bits.  ``generate`` refuses to run on a host whose
-torch.exp disagrees with that sample, and refuses a result whose hash is not
-GOLDEN_SHA256; ``read`` refuses a table whose hash is not GOLDEN_SHA256.  So a
-table that would silently move the decoded boxes cannot be built or loaded.
+tests/golden/*).  Its PAYLOAD -- record count, domain, offsets and keys, not
+the informational torch-version / CPU header strings -- hashes to
+GOLDEN_PAYLOAD_SHA256, checked by ``expand``, ``generate``, ``verify`` and
+``read``; a table that would silently move the decoded boxes cannot be built
+or loaded.  ``exp_sample.npz`` (committed) holds 16384 inputs -- half of them
+recorded exceptions -- with the golden host's torch.exp bits; ``generate``
+(re-deriving the table from torch.exp itself) refuses to run on a host whose
+torch.exp disagrees with that sample.
 """
 from __future__ import annotations
 
@@ -51,11 +56,18 @@ from ._lib import TMRError
 MAGIC = b"TMRXEXP1"
 HEADER = 128
 DOMAIN = (2.0 ** -26, 128.0)
-PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "exp_ref.bin")
-SAMPLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "exp_sample.npz")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PATH = os.path.join(_HERE, "exp_ref.bin")
+BLOB = os.path.join(_HERE, "exp_ref.rc")
+SAMPLE = os.path.join(_HERE, "exp_sample.npz")
 # the host that generated tests/golden/* (oracle/make_golden.py) and its table
 GOLDEN_CPU = "Intel(R) Xeon(R) Processor"
-GOLDEN_SHA256 = "f88106cc9a510176b0d89d1004e636bd8df2d91c1ea45969f44dace303e1b1de"
+GOLDEN_TORCH = "2.10.0+rocm7.0"
+GOLDEN_COUNT = 9459739
+GOLDEN_PAYLOAD_SHA256 = "f81112962e3f17bdb942560beacd7779eb3e491a38561ce79e8003c2203bd8f7"
+# whole file as expand() writes it (header strings GOLDEN_TORCH / GOLDEN_CPU);
+# informational -- the pin is the payload hash
+GOLDEN_FILE_SHA256 = "f88106cc9a510176b0d89d1004e636bd8df2d91c1ea45969f44dace303e1b1de"
 
 _lock = threading.Lock()
 _dev_cache = {}
@@ -86,6 +98,16 @@ def sha256(path: str = PATH) -> str:
     return h.hexdigest()
 
 
+def payload_sha256(raw: np.ndarray) -> str:
+    """SHA-256 of what the decode reads: count + domain (header bytes 8..23)
+    and everything after the header.  The torch-version and CPU strings are
+    informational and not hashed."""
+    h = hashlib.sha256()
+    h.update(raw[8:24].tobytes())
+    h.update(raw[HEADER:].tobytes())
+    return h.hexdigest()
+
+
 def host_matches_golden(sample: str = SAMPLE) -> tuple:
     """(ok, mismatches, n): does this host's torch.exp (CPU fp32) give the
     golden host's bits on the committed sample?"""
@@ -98,10 +120,9 @@ def host_matches_golden(sample: str = SAMPLE) -> tuple:
 
 def make_sample(path: str = PATH, out: str = SAMPLE, n: int = 8192, seed: int = 11) -> None:
     """Write the committed sample from a table known to be the golden one
-    (GOLDEN_SHA256): n recorded inputs + n other inputs of the domain, with
+    (GOLDEN_PAYLOAD_SHA256): n recorded inputs + n other inputs of the domain, with
     this (golden) host's torch.exp bits."""
-    if sha256(path) != GOLDEN_SHA256:
-        raise TMRError("make_sample needs the golden table")
+    verify(path)
     rec = recorded_inputs(np.fromfile(path, dtype=np.uint8))
     rng = np.random.default_rng(seed)
     a = rng.choice(rec, n, replace=False)
@@ -113,34 +134,90 @@ def make_sample(path: str = PATH, out: str = SAMPLE, n: int = 8192, seed: int = 
     np.savez_compressed(out, x=x, y=y)
 
 
+def _write(exc: np.ndarray, path: str, torch_version: str, cpu: str) -> None:
+    """Write the table of the sorted recorded inputs `exc` to `path` (via a
+    temporary name); raises unless its payload is the golden one."""
+    hi16 = (exc >> np.uint32(16)).astype(np.int64)
+    offsets = np.searchsorted(hi16, np.arange(65537), side="left").astype(np.uint32)
+    lo16 = (exc & np.uint32(0xFFFF)).astype(np.uint16)
+    ver = torch_version.encode()[:32].ljust(32, b"\0")
+    lo_b = int(np.float32(DOMAIN[0]).view(np.uint32))
+    hi_b = int(np.float32(DOMAIN[1]).view(np.uint32))
+    head = MAGIC + struct.pack("<QII", exc.size, lo_b, hi_b) + ver + cpu.encode()[:64].ljust(64, b"\0")
+    head = head.ljust(HEADER, b"\0")
+    raw = np.concatenate([np.frombuffer(head, np.uint8), offsets.view(np.uint8), lo16.view(np.uint8)])
+    got = payload_sha256(raw)
+    if got != GOLDEN_PAYLOAD_SHA256:
+        raise TMRError(f"reference-exp table payload sha256 {got} is not the golden "
+                       f"{GOLDEN_PAYLOAD_SHA256}; {path} not written")
+    tmp = path + ".tmp"
+    raw.tofile(tmp)
+    os.replace(tmp, path)
+
+
 def generate(path: str = PATH) -> int:
+    """Re-derive the table from this host's torch.exp (only on a host whose
+    torch.exp is the golden host's, checked on the committed sample)."""
     ok, bad, n = host_matches_golden()
     if not ok:
         raise TMRError(f"this host's torch.exp ({host_cpu()}, torch {torch.__version__}) differs from "
                        f"the golden host's ({GOLDEN_CPU}) on {bad} of {n} committed samples "
-                       f"(exp_sample.npz): the reference-exp table cannot be generated here. Copy "
-                       f"exp_ref.bin (sha256 {GOLDEN_SHA256}) from a build on the golden host.")
+                       f"(exp_sample.npz): the reference-exp table cannot be generated here; "
+                       f"expand() it from the committed {os.path.basename(BLOB)}")
     exc = exceptions()
-    hi16 = (exc >> np.uint32(16)).astype(np.int64)
-    offsets = np.searchsorted(hi16, np.arange(65537), side="left").astype(np.uint32)
-    lo16 = (exc & np.uint32(0xFFFF)).astype(np.uint16)
-    ver = torch.__version__.encode()[:32].ljust(32, b"\0")
-    lo_b = int(np.float32(DOMAIN[0]).view(np.uint32))
-    hi_b = int(np.float32(DOMAIN[1]).view(np.uint32))
-    head = MAGIC + struct.pack("<QII", exc.size, lo_b, hi_b) + ver + host_cpu().encode()[:64].ljust(64, b"\0")
-    head = head.ljust(HEADER, b"\0")
-    tmp = path + ".tmp"
-    with open(tmp, "wb") as fh:
-        fh.write(head)
-        fh.write(offsets.tobytes())
-        fh.write(lo16.tobytes())
-    got = sha256(tmp)
-    if got != GOLDEN_SHA256:
-        os.remove(tmp)
-        raise TMRError(f"generated reference-exp table has sha256 {got}, not the golden {GOLDEN_SHA256} "
-                       f"(torch {torch.__version__} on {host_cpu()}); not installed")
-    os.replace(tmp, path)
+    _write(exc, path, torch.__version__, host_cpu())
     return int(exc.size)
+
+
+def _codec():
+    from . import _lib
+    return _lib.load()
+
+
+def compress(path: str = PATH, out: str = BLOB) -> int:
+    """Write the committed compact form of the golden table (csrc/exp_codec.cpp)."""
+    exc = np.ascontiguousarray(recorded_inputs(read(path)), np.uint32)
+    lib = _codec()
+    n = lib.tmr_exp_table_encode(exc.ctypes.data, exc.size, None, 0)
+    if n < 0:
+        raise TMRError(f"tmr_exp_table_encode failed (rc={n})")
+    buf = np.zeros(n, np.uint8)
+    if lib.tmr_exp_table_encode(exc.ctypes.data, exc.size, buf.ctypes.data, n) != n:
+        raise TMRError("tmr_exp_table_encode failed")
+    tmp = out + ".tmp"
+    buf.tofile(tmp)
+    os.replace(tmp, out)
+    return int(n)
+
+
+def expand(blob: str = BLOB, path: str = PATH) -> int:
+    """Build the table from the committed compact form; host independent, and
+    the result must hash to GOLDEN_PAYLOAD_SHA256."""
+    if not os.path.exists(blob):
+        raise TMRError(f"{blob} missing: the committed compact reference-exp table")
+    buf = np.fromfile(blob, dtype=np.uint8)
+    lib = _codec()
+    n = lib.tmr_exp_table_decode(buf.ctypes.data, buf.size, None, 0)
+    if n != GOLDEN_COUNT:
+        raise TMRError(f"{blob}: records {n} inputs, not the golden {GOLDEN_COUNT}")
+    exc = np.zeros(n, np.uint32)
+    if lib.tmr_exp_table_decode(buf.ctypes.data, buf.size, exc.ctypes.data, n) != n:
+        raise TMRError(f"{blob}: malformed compact reference-exp table")
+    _write(exc, path, GOLDEN_TORCH, GOLDEN_CPU)
+    _verified.pop(path, None)
+    return int(n)
+
+
+def ensure(path: str = PATH) -> str:
+    """build(): keep a table whose payload is golden, else expand the blob."""
+    if os.path.exists(path):
+        try:
+            verify(path)
+            return "verified"
+        except TMRError:
+            pass
+    expand(path=path)
+    return "expanded"
 
 
 def host_cpu() -> str:
@@ -162,16 +239,20 @@ _verified = {}
 
 
 def verify(path: str = PATH) -> None:
-    """Raise unless `path` is the golden table (GOLDEN_SHA256); once per
-    (path, mtime) per process."""
+    """Raise unless `path` holds the golden table (GOLDEN_PAYLOAD_SHA256 over
+    its payload; the header strings may differ); once per (path, mtime) per
+    process."""
     key = (path, os.path.getmtime(path))
     if _verified.get(path) == key:
         return
-    got = sha256(path)
-    if got != GOLDEN_SHA256:
-        raise TMRError(f"{path}: sha256 {got} is not the golden reference-exp table {GOLDEN_SHA256} "
-                       f"(recorded on {GOLDEN_CPU}); rebuild with __graft_entry__.build() on a host "
-                       "whose torch.exp matches exp_sample.npz")
+    raw = np.fromfile(path, dtype=np.uint8)
+    if raw.size < HEADER or raw[:8].tobytes() != MAGIC:
+        raise TMRError(f"{path}: not a reference-exp table")
+    got = payload_sha256(raw)
+    if got != GOLDEN_PAYLOAD_SHA256:
+        raise TMRError(f"{path}: payload sha256 {got} is not the golden reference-exp table "
+                       f"{GOLDEN_PAYLOAD_SHA256} (recorded on {GOLDEN_CPU}); rebuild it with "
+                       "__graft_entry__.build(), which expands the committed exp_ref.rc")
     _verified[path] = key
 
 
@@ -179,11 +260,8 @@ def read(path: str = PATH) -> np.ndarray:
     if not os.path.exists(path):
         raise TMRError(f"{path} missing: the reference-exp table is built by "
                        "`python -c 'import __graft_entry__ as g; g.build()'`")
-    raw = np.fromfile(path, dtype=np.uint8)
-    if raw[:8].tobytes() != MAGIC:
-        raise TMRError(f"{path}: not a reference-exp table")
     verify(path)
-    return raw
+    return np.fromfile(path, dtype=np.uint8)
 
 
 def recorded_inputs(raw: np.ndarray) -> np.ndarray:

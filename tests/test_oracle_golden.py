@@ -1,12 +1,15 @@
 """Pins the CPU oracle (oracle/) against golden vectors produced by the
 reference itself (oracle/make_golden.py).  CPU only."""
 import json
+import os
 
 import numpy as np
 import pytest
 import torch
 
 import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def normwise(a, b):
@@ -188,14 +191,15 @@ def test_reference_exp_characterised():
 
 
 def test_reference_exp_table_pinned(tmp_path, monkeypatch):
-    """The reference-exp table is the golden host's: its SHA-256 is pinned,
-    this host's torch.exp matches the committed golden sample, a different
-    table is refused by read(), and generation refuses a host whose torch.exp
-    differs from the golden host's (VERDICT r2 #4)."""
+    """The reference-exp table is the golden host's: its payload SHA-256 is
+    pinned, this host's torch.exp matches the committed golden sample on the
+    golden host, a different table is refused by read(), a table differing
+    only in its informational header strings is accepted, and
+    generation refuses a host whose torch.exp differs from the golden host's."""
     from tmr_amd import exp_table
     from tmr_amd._lib import TMRError
-    assert exp_table.sha256() == exp_table.GOLDEN_SHA256
     raw = exp_table.read()
+    assert exp_table.payload_sha256(raw) == exp_table.GOLDEN_PAYLOAD_SHA256
     assert exp_table.recorded_cpu(raw) == exp_table.GOLDEN_CPU
     ok, bad, n = exp_table.host_matches_golden()
     if exp_table.host_cpu() == exp_table.GOLDEN_CPU:
@@ -214,12 +218,47 @@ def test_reference_exp_table_pinned(tmp_path, monkeypatch):
     bad_copy.write_bytes(bytes(b))
     with pytest.raises(TMRError, match="sha256"):
         exp_table.read(str(bad_copy))
+    # another torch build / CPU name in the header only: accepted
+    other = tmp_path / "other_header.bin"
+    b = bytearray(open(exp_table.PATH, "rb").read())
+    b[24:56] = b"9.9.9+other".ljust(32, b"\0")
+    b[56:120] = b"Some Other CPU".ljust(64, b"\0")
+    other.write_bytes(bytes(b))
+    assert exp_table.payload_sha256(exp_table.read(str(other))) == exp_table.GOLDEN_PAYLOAD_SHA256
     # another host's exp: generation refuses before writing anything
     monkeypatch.setattr(exp_table, "host_matches_golden", lambda sample=None: (False, 17, 16384))
     out = tmp_path / "gen.bin"
     with pytest.raises(TMRError, match="differs from the golden host"):
         exp_table.generate(str(out))
     assert not out.exists()
+
+
+def test_reference_exp_table_from_committed_blob(tmp_path):
+    """the table a clean checkout builds.  The compact form as
+    COMMITTED at HEAD (git show, not the working tree) expands -- with no use
+    of this host's torch.exp -- to the pinned payload, byte-identical to the
+    golden host's table; a damaged blob is refused."""
+    import subprocess
+    from tmr_amd import exp_table
+    from tmr_amd._lib import TMRError
+    rel = os.path.relpath(exp_table.BLOB, REPO)
+    try:
+        blob = subprocess.run(["git", "-C", REPO, "show", f"HEAD:{rel}"], check=True,
+                              capture_output=True).stdout
+    except (OSError, subprocess.CalledProcessError):
+        pytest.skip("not a git checkout")
+    src = tmp_path / "exp_ref.rc"
+    src.write_bytes(blob)
+    out = tmp_path / "exp_ref.bin"
+    assert exp_table.expand(str(src), str(out)) == exp_table.GOLDEN_COUNT
+    assert exp_table.payload_sha256(np.fromfile(out, np.uint8)) == exp_table.GOLDEN_PAYLOAD_SHA256
+    assert exp_table.sha256(str(out)) == exp_table.GOLDEN_FILE_SHA256
+    bad = bytearray(blob)
+    bad[len(bad) // 2] ^= 0x10
+    src.write_bytes(bytes(bad))
+    with pytest.raises(TMRError):
+        exp_table.expand(str(src), str(tmp_path / "bad.bin"))
+    assert not (tmp_path / "bad.bin").exists()
 
 
 HEADER_FLIP = 128 + 4 * 40000  # a byte inside the offsets block
