@@ -18,6 +18,17 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_csv import summarize  # noqa: E402
 
+
+def _buildinfo():
+    """tmr_amd/buildinfo.py loaded by path (no torch, no package import)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "template-matching-and-regression-mapreduce_amd", "buildinfo.py")
+    spec = importlib.util.spec_from_file_location("tmr_buildinfo", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
 # role -> kernel regex (rocprofv3 CSV names are demangled for the split and
 # rows kernels, mangled for the MFMA correlation)
 ROLES = {
@@ -53,6 +64,9 @@ def main(pmc_dir, label, out):
             c = r["counters"]
             if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("GRBM_GUI_ACTIVE"):
                 r["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            # the tree the counters belong to: bench.py prints them only
+            # while the kernel's sources are unchanged
+            r["source_digest"] = _buildinfo().source_digest(role)
             rec[role] = r
         res["configs"][cfg] = rec
     with open(out, "w") as fh:
