@@ -275,7 +275,6 @@ def main():
     ap.add_argument("--exemplars", type=int, default=None)
     ap.add_argument("--precision", default=None, choices=sorted(SPLIT_TERMS),
                     help="decoder arithmetic (default: the config's; fp32 = 3-term fp16 split)")
-    ap.add_argument("--decoder", default="split", choices=["split", "wino", "direct"])
     ap.add_argument("--path", default="detect", choices=["detect", "module"],
                     help="detect: TMREngine.detect over the batch (B x E units per launch); module: "
                          "the reference's per-exemplar module calls (demo.py:106-130)")
@@ -290,7 +289,7 @@ def main():
     a = ap.parse_args()
     # the committed PMC records describe each config's own workload only
     own_options = (a.batch is None and a.exemplars is None and a.precision is None
-                   and a.decoder == "split" and a.path == "detect")
+                   and a.path == "detect")
 
     rank, world, local = driver.dist_env()
     # one process per GPU; a rehearsal with more ranks than GPUs (gloo on a
@@ -312,7 +311,6 @@ def main():
     P = synth.reference_state_dict(0, device=dev)
     prec = a.precision or cfg.get("precision", "fp32")
     eng = tmr.TMREngine(P, tmr.PathConfig(precision=prec))
-    eng.decoder_algo = a.decoder
     # A/B knob: TMR_BENCH_OUT_BF16=0 keeps the bf16 contract's f_TM plane in fp32
     eng.out_bf16 = os.environ.get("TMR_BENCH_OUT_BF16", "1") != "0"
     B = a.batch or cfg["batch"]
@@ -395,27 +393,16 @@ def main():
         avg_s = float(np.mean(dec_ms)) / 1e3
         achieved = flops / avg_s / 1e12
         algo = eng.last_decoder_algo
-        peak, terms = FP32_PEAK_TFLOPS, 1
-        if algo == "split":
-            terms = SPLIT_TERMS[prec]
-            peak = F16_PEAK_TFLOPS
-            kernel_name = ("tmr_split_conv_heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
-                           "+ LeakyReLU + 1x1 heads, v_mfma_f32_16x16x32_%s)"
-                           % ("bf16" if prec == "bf16" else "f16"))
-            flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
-                           "(%s; the fp half runs once per image in tmr_split_conv_store and is "
-                           "shared by its exemplars; unshared (E=1): K=(256+512)*9, the fp half folded through input_proj)"
-                           % (terms, "fp32-grade 3-term fp16 split: hi*hi + lo*hi + hi*lo"
-                              if terms == 3 else "one %s term" % prec))
-        elif algo == "wino":
-            kernel_name = ("tmr_wino_conv_heads (Winograd F(2x2,3x3) decoder_b+decoder_o f_TM half "
-                           "+ LeakyReLU + 1x1 heads, fp32 MFMA 32x32x2)")
-            flops_basis = ("executed: 16 transform-domain GEMMs, 2*16*(H/2*W/2)*N(2048)*K per unit "
-                           "(K=512: the fp half runs once per image in tmr_wino_conv_store and is "
-                           "shared by its exemplars; K=1024 when E=1)")
-        else:
-            kernel_name = "tmr_conv_heads (direct decoder_b+decoder_o f_TM half + heads)"
-            flops_basis = "executed: 2*H*W*N(2048)*K(512*9) per unit (f_TM half)"
+        terms = SPLIT_TERMS[prec]
+        peak = F16_PEAK_TFLOPS
+        kernel_name = ("tmr_split_conv_heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
+                       "+ LeakyReLU + 1x1 heads, v_mfma_f32_16x16x32_%s)"
+                       % ("bf16" if prec == "bf16" else "f16"))
+        flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
+                       "(%s; the fp half runs once per image in tmr_split_conv_store and is "
+                       "shared by its exemplars; unshared (E=1): K=(256+512)*9, the fp half folded through input_proj)"
+                       % (terms, "fp32-grade 3-term fp16 split: hi*hi + lo*hi + hi*lo"
+                          if terms == 3 else "one %s term" % prec))
         executed_achieved = achieved * terms
         # SURVEY.md 8d algorithmic FLOPs of the timed launch: the decoder
         # convs' f_TM half, 2*H*W*2048*(512*9) per unit (both halves when the

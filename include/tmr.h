@@ -66,24 +66,8 @@ typedef struct tmr_peak_param {
 int tmr_version(void);
 const char *tmr_strerror(int rc);
 
-/* ---- weights ---------------------------------------------------------
- * Pack conv weights W[N][C][ks][ks] (PyTorch layout) for the MFMA conv
- * kernels: wpack is [ceil(N/128)][ceil(C/cc)][ks*ks][cc][128] fp32, zero
- * padded.  Size in floats from tmr_conv_pack_size().  Replaces nothing in the
- * reference (a derived cache of nn.Conv2d.weight, regression_head.py:7 and
- * matching_net.py:27-30). */
-int64_t tmr_conv_pack_size(int N, int C, int ks);
-int tmr_conv_pack(const float *w, int N, int C, int ks, float *wpack, void *stream);
-
-/* ---- (a2+a3) bilinear x2 upsample fused into the 1x1 input projection -----
- * fp[b] = W_proj * up2x(feat[b]) + bias   (models/matching_net.py:50-51,56)
- * feat [B,Cin,Hin,Win]; fp [B,N,H,W] with H=2*Hin (upsample!=0) or H=Hin.
- * f0 (nullable) receives up2x(feat) [B,Cin,H,W] (the API output f[0], :81). */
-int tmr_upsample_proj(const float *feat, int B, int Cin, int Hin, int Win, int upsample,
-                      const float *wpack, const float *bias, int N, float *fp, float *f0,
-                      void *stream);
-
-/* f[0] = F.interpolate(feat, scale_factor=2, mode='bilinear',
+/* ---- (a2+a13) bilinear x2 upsample ---------------------------------------
+ * f[0] = F.interpolate(feat, scale_factor=2, mode='bilinear',
  * align_corners=False) alone (matching_net.py:50-51, the API output :81):
  * feat [BC][Hin][Win] -> out [BC][2 Hin][2 Win], bit-exact with ATen's CPU
  * kernel's fma nesting. */
@@ -181,56 +165,27 @@ int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, i
 int tmr_template_split_prec(const float *templates, const tmr_unit_t *units, int U, int C,
                             int64_t total_rows, int prec, void *out, void *stream);
 
-/* ---- (a10+a11+a12) conv stack ---------------------------------------------
- * Implicit-GEMM kxk conv over the virtual channel concat
- *   x_u = cat([src0[unit_image[u]] (C0 ch), src1[u] (C1 ch)])   (matching_net.py:64)
- * with bias and optional LeakyReLU(0.01) (regression_head.py:7-8), fp32 MFMA.
- * unit_image (device int32[U]) may be NULL (identity).
- * tmr_conv_store: out [U,N,H,W].
- * tmr_conv_heads: the fused decoder+1x1-head epilogue; out is never stored.
- *   acc_init (nullable, [img][N][H][W] indexed by unit_image) is added to the
- *   accumulators before the K loop: with it the decoder's fp half
- *   (conv over src0 = fp, computed once per image by tmr_conv_store) is shared
- *   by the image's exemplars and only the f_TM half runs per unit:
- *   partials[t][j][u][h][w] += sum_{n in tile t} act(conv)[n] * headw[n][j], j<5
- *   (headw [ceil(N/128)*128][5] fp32, zero padded; j 0-3 = ltrbs_head,
- *   4 = objectness_head,
- *   regression_head.py:31,50) and tmr_heads_reduce() adds the head biases. */
-int tmr_conv_store(const float *src0, int C0, const int32_t *unit_image, const float *src1,
-                   int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
-                   int ks, int leaky, float *out, void *stream);
-int tmr_conv_heads(const float *src0, int C0, const int32_t *unit_image, const float *src1,
-                   int C1, int U, int H, int W, const float *wpack, const float *bias, int N,
-                   int ks, int leaky, const float *headw, const float *acc_init,
-                   float *partials, void *stream);
+/* ---- (a10+a11+a12) conv stack: head partials ------------------------------
+ * tmr_split_conv_heads (below) never stores the decoder activations: each
+ * 128-channel tile t of the fused decoder_b || decoder_o GEMM writes
+ *   partials[t][j][u][h][w] = sum_{n in tile t} act(conv)[n] * headw[n][j], j < 5
+ * (headw [ceil(N/128)*128][5] fp32, zero padded; j 0-3 = ltrbs_head,
+ * 4 = objectness_head, regression_head.py:31,50), and tmr_heads_reduce() sums
+ * the tiles and adds the head biases.  Size in floats: */
 int64_t tmr_heads_partials_size(int N, int U, int H, int W);
 /* o [U,1,H,W] = head_bias[4] + sum_t partials[t][4];  b [U,4,H,W] (nullable) =
  * head_bias[j] + sum_t partials[t][j], t over ceil(N/tile_n) channel tiles
- * (tile_n = 128 for tmr_conv_heads, 64 for tmr_wino_conv_heads). */
+ * (tile_n = 128, the split kernel's tile; 64 is accepted too). */
 int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int W,
                      const float *head_bias, float *o, float *b, void *stream);
 
-/* ---- (a11) Winograd F(2x2,3x3) variant of the 3x3 decoder conv -------------
- * Same semantics as tmr_conv_store / tmr_conv_heads for ks = 3 (pad 1), with
- * 16 instead of 36 multiplies per 2x2 output tile (fp32 MFMA; fp32 transforms,
- * same 1e-5 contract).  upack = U = G g G^T packed by tmr_wino_pack:
- * [ceil(N/64)][ceil(C/8)][16 xi][2][64 n][4] fp32 (chunk channel c = 2*k4 + k2).  acc_init (nullable, [img][N][H][W])
- * is added to the conv result before bias/activation in both variants. */
-int64_t tmr_wino_pack_size(int N, int C);
-int tmr_wino_pack(const float *w, int N, int C, float *upack, void *stream);
-int tmr_wino_conv_store(const float *src0, int C0, const int32_t *unit_image, const float *src1,
-                        int C1, int U, int H, int W, const float *upack, const float *bias, int N,
-                        int leaky, const float *acc_init, float *out, void *stream);
-int tmr_wino_conv_heads(const float *src0, int C0, const int32_t *unit_image, const float *src1,
-                        int C1, int U, int H, int W, const float *upack, const float *bias, int N,
-                        int leaky, const float *headw, const float *acc_init, float *partials,
-                        void *stream);
-
-/* ---- (a11) split-precision 16-bit-MFMA variant of the decoder conv ---------
- * Direct implicit-GEMM kxk conv (ks 1/3/5/7, pad ks/2) on
- * v_mfma_f32_16x16x32_{f16,bf16}; same semantics as tmr_conv_store /
- * tmr_conv_heads (regression_head.py:7-8, matching_net.py:63-75) except that
- * operands are pre-packed 16-bit records:
+/* ---- (a11) the decoder conv: split-precision 16-bit MFMA -------------------
+ * Direct implicit-GEMM kxk conv (ks 1/3/5/7, pad ks/2) over the virtual
+ * channel concat x_u = cat([src0[unit_image[u]] (C0 ch), src1[u] (C1 ch)])
+ * (matching_net.py:64) with bias and optional LeakyReLU(0.01)
+ * (regression_head.py:7-8) on v_mfma_f32_16x16x32_{f16,bf16}; unit_image
+ * (device int32[U]) may be NULL (identity).  Operands are pre-packed 16-bit
+ * records:
  *   TMR_PREC_F16X3: x*s = xh + xl, w*s' = wh + wl (fp16, power-of-two scales
  *                   from the tensors' max |.|), x.w = (wh xh + wl xh + wh xl)
  *                   / (s s') with fp32 accumulation: the fp32 path's 1e-5

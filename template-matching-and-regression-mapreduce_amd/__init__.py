@@ -8,7 +8,7 @@ for gfx950); there is no CPU fallback.
 from . import host, synth  # noqa: F401
 from ._lib import LIB_PATH, TMRError, load  # noqa: F401
 from .backbone import FeatureInput, build_backbone, register_backbone, unregister_backbone  # noqa: F401
-from .engine import PathConfig, TMREngine, conv2d, pack_conv  # noqa: F401
+from .engine import PathConfig, TMREngine, conv2d_split  # noqa: F401
 from .matching_net import Backbone_Encoder, build_encoder, build_model, matching_net  # noqa: F401
 from .regression_head import BboxesHead, Decoder_model, ObjectnessHead  # noqa: F401
 from .template_matching import TemplateMatching  # noqa: F401

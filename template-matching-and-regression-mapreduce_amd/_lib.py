@@ -56,9 +56,6 @@ _D = ctypes.c_double
 SIGNATURES = {
     "tmr_version": (_I, []),
     "tmr_strerror": (ctypes.c_char_p, [_I]),
-    "tmr_conv_pack_size": (_L, [_I, _I, _I]),
-    "tmr_conv_pack": (_I, [_P, _I, _I, _I, _P, _P]),
-    "tmr_upsample_proj": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P]),
     "tmr_upsample2x": (_I, [_P, _I, _I, _I, _P, _P]),
     "tmr_templates": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tmr_xcorr": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
@@ -71,14 +68,8 @@ SIGNATURES = {
     "tmr_template_split_size": (_L, [_I, _I, _L]),
     "tmr_template_split": (_I, [_P, _P, _I, _I, _L, _P, _P]),  # (..., total_rows, out, stream)
     "tmr_template_split_prec": (_I, [_P, _P, _I, _I, _L, _I, _P, _P]),  # (..., total_rows, prec, out, stream)
-    "tmr_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P]),
-    "tmr_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),
     "tmr_heads_reduce": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
-    "tmr_wino_pack_size": (_L, [_I, _I]),
-    "tmr_wino_pack": (_I, [_P, _I, _I, _P, _P]),
-    "tmr_wino_conv_store": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P]),
-    "tmr_wino_conv_heads": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "tmr_absmax": (_I, [_P, _L, _I, _P, _P]),
     "tmr_split_xpack_size": (_L, [_I, _I, _I, _I, _I, _I]),
     "tmr_split_xpack": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -66,39 +66,18 @@ typedef __attribute__((address_space(3))) void *lds_ptr_t;
 // r02an), wave priority over the MFMA stream (no change, r02av).
 
 constexpr int BM = 128;      // output channels per block
-#ifndef TMR_SPLIT_TH  // output rows per block (8: with TMR_SPLIT_NW=4 and a halved LDS budget, two
-#define TMR_SPLIT_TH 16 // co-resident blocks per CU, measured as a variant: DESIGN.md 4.2)
-#endif
-#ifndef TMR_SPLIT_LDS_KB  // LDS budget per block
-#define TMR_SPLIT_LDS_KB 160
-#endif
-constexpr int TH = TMR_SPLIT_TH;
+constexpr int TH = 16;       // output rows per block
 constexpr int TW = 32;       // output cols per block
+// LDS budget per block: the whole CU (one block per CU).  TH = 8 with 4 waves
+// and 80 KB, two co-resident blocks per CU, was 14-17% slower
+constexpr int LDS_KB = 160;
+// XCD block groups: PXG pixel tiles x NG channel tiles per XCD wave of 32
+// co-resident blocks (8 x 4 minimises the wave's distinct operands, r03ab)
+constexpr int PXG = 8, NG = 4;
 // waves per block: 8 (2 along n x 4 along rows, 128 accumulator VGPRs, two
-// waves per SIMD) or 4 (1 x 4, 256 accumulators, one wave per SIMD: half
-// the LDS fragment reads per MFMA)
-#ifndef TMR_SPLIT_PXG  // XCD block groups: pixel tiles x channel tiles
-#define TMR_SPLIT_PXG 8
-#endif
-#ifndef TMR_SPLIT_NG
-#define TMR_SPLIT_NG 4
-#endif
-#ifndef TMR_SPLIT_ACC_NT  // non-temporal stores of the tiled acc0 (read back by a later launch; +0.4% config B)
-#define TMR_SPLIT_ACC_NT 1
-#endif
-#ifndef TMR_SPLIT_HOIST_HOFF  // halo DMA per-lane offsets computed once (VGPRs) instead of per DMA
-#define TMR_SPLIT_HOIST_HOFF 1
-#endif
-#ifndef TMR_XPACK4  // activation records 4 pixels per thread (xpack4_kernel)
-#define TMR_XPACK4 1
-#endif
-#ifndef TMR_SPLIT_LO3  // F16X3 lo half-chunks in longer steps (see Geo::LO3)
-#define TMR_SPLIT_LO3 1
-#endif
-#ifndef TMR_SPLIT_NW
-#define TMR_SPLIT_NW 8
-#endif
-constexpr int NWAVES = TMR_SPLIT_NW;
+// waves per SIMD); the code also holds the 4-wave form (1 x 4, 256
+// accumulators, one wave per SIMD), measured 17% slower (r02ah)
+constexpr int NWAVES = 8;
 constexpr int NTHREADS = NWAVES * 64;
 constexpr int WNS = (NWAVES == 8 || TH == 8) ? 2 : 1;  // waves along n
 static_assert(TH == 4 * NWAVES / WNS, "a wave owns 4 output rows");
@@ -218,9 +197,8 @@ struct Geo {
     static constexpr int HB = MPW * NWAVES * 1024;
     static constexpr int NPLW = Prec<PREC>::WREC / 16;         // weight planes per tap (8 or 4)
     static constexpr int WB1 = NPLW * WPL;                     // weight bytes per tap
-    // (a reduced budget applies to the 3x3 decoders; larger kernels keep the CU's 160 KB)
     static constexpr bool fits(int tps, int nwb) {
-        return 2 * HB + nwb * tps * WB1 <= (KS <= 3 ? TMR_SPLIT_LDS_KB : 160) * 1024;
+        return 2 * HB + nwb * tps * WB1 <= LDS_KB * 1024;
     }
     // taps per barrier step and weight buffers (DMA lookahead NWB-1 steps)
     static constexpr int TPS = T == 1 ? 1 : fits(3, 2) ? 3 : fits(2, 2) ? 2 : 1;
@@ -234,7 +212,7 @@ struct Geo {
     // steps per chunk (10 -> 8).  One weight lookahead step (NWB == 2) only.
     // Measured (r02bm, A/B in one call): fp32 heads 28.02/28.17 -> 27.89/27.97
     // ms per 48 units, config B 451.3/451.5 -> 454.4/454.1 images/s.
-    static constexpr bool LO3 = TMR_SPLIT_LO3 && PREC == TMR_PREC_F16X3 && NWB == 2 && T > 1;
+    static constexpr bool LO3 = PREC == TMR_PREC_F16X3 && NWB == 2 && T > 1;
     static constexpr int SPCL = LO3 ? (T + 2 * TPS - 1) / (2 * TPS) : SPC;
     static constexpr int TPSL = LO3 ? (T + SPCL - 1) / SPCL : TPS;
     static constexpr int SPCC = Prec<PREC>::HALVES == 2 ? SPC + SPCL : SPC;  // steps per chunk
@@ -309,7 +287,6 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     int nt, mt, u;
     {
         // one XCD wave of 32 blocks = PXG pixel tiles x NG channel tiles
-        constexpr int PXG = TMR_SPLIT_PXG, NG = TMR_SPLIT_NG;
         const int per_unit = a.NT * a.MT;
         u = L / per_unit;
         const int r = L - u * per_unit;
@@ -335,14 +312,11 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 
     // Per-lane halo DMA source of wave-instruction m (half-chunk invariant):
     // LDS piece e of the halo image is plane e / NPIX, record e % NPIX; pad
-    // records re-read a legal address.  Recomputed per DMA (a few VALU)
-    // rather than held in registers through the main loop.
+    // records re-read a legal address.  The compiler hoists the MPW offsets
+    // out of the main loop into VGPRs (r02ao: a per-DMA dependent VALU chain
+    // had sat in the waves' in-order MFMA issue stream).
     auto hoff = [&](int m) -> int {
-        int ln = lane;
-#if !TMR_SPLIT_HOIST_HOFF
-        asm volatile("" : "+v"(ln));  // opaque: keeps LICM from hoisting (and spilling) the offsets
-#endif
-        const int e = (wave + NWAVES * m) * 64 + ln;
+        const int e = (wave + NWAVES * m) * 64 + lane;
         int q = e / NPIX, p = e % NPIX;
         if (q >= P || p >= G::HR * HC) q = p = 0;
         const int hy = p / HC, hx = p % HC;
@@ -633,10 +607,8 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         for (int in = 0; in < NIN; ++in)
 #pragma unroll
             for (int jp = 0; jp < 8; ++jp) {
-                if (TMR_SPLIT_ACC_NT)
-                    __builtin_nontemporal_store(acc[in][jp] * inv, o + (in * 8 + jp) * 64);
-                else
-                    o[(in * 8 + jp) * 64] = acc[in][jp] * inv;
+                // non-temporal: read back by a later launch (+0.4% config B)
+                __builtin_nontemporal_store(acc[in][jp] * inv, o + (in * 8 + jp) * 64);
             }
         return;
     }
@@ -880,16 +852,8 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
 // pixel-contiguous (1 KB per wave store).  Blocks past `nseg` write the
 // padding ring (zero records: the split of 0 is 0 in every term).  Records
 // are bit-identical to xpack_kernel<PREC, 0>'s.
-#ifndef TMR_XSEG
-#define TMR_XSEG 128
-#endif
-#ifndef TMR_XPACK4_3T  // 3-term records on xpack4_kernel too (measured slower, r02bo3)
-#define TMR_XPACK4_3T 0
-#endif
-constexpr int XSEG = TMR_XSEG;
-#ifndef TMR_XPACK16_RPB  // rows per block of the bf16-input record pack
-#define TMR_XPACK16_RPB 4
-#endif
+constexpr int XSEG = 128;
+constexpr int XPACK16_RPB = 4;  // rows per block of the bf16-input record pack (1/4/8: r03s)
 // IN: the activation's element type, float or __bf16 (a bf16 f_TM plane from
 // tmr_xcorr_out: bf16 records of it are its own elements, tmr_split_xpack16);
 // RPB rows of the segment per block (the bf16 form moves half the bytes per
@@ -1093,16 +1057,10 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
     // one-term records from LDS-transposed row segments (bf16 0.61 -> 0.50 ms
     // per 48 units at 128^2, r02bo3); the 3-term records stay on the
     // one-pixel kernel (0.61 vs 0.73 ms: twice the stores per staged byte)
-    if (TMR_XPACK4 && MODE == 0 && W % 4 == 0 && (TMR_XPACK4_3T || prec != TMR_PREC_F16X3)) {
+    if (MODE == 0 && W % 4 == 0 && prec != TMR_PREC_F16X3) {
         const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
         const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
         switch (prec) {
-#if TMR_XPACK4_3T
-            case TMR_PREC_F16X3:
-                hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_F16X3>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
-                                   ks / 2, nseg, nbord, xmax, static_cast<h8 *>(out));
-                break;
-#endif
             case TMR_PREC_BF16:
                 hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_BF16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
                                    ks / 2, nseg, nbord, nullptr, static_cast<b8 *>(out));
@@ -1170,7 +1128,7 @@ extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int 
                                  void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec == TMR_PREC_BF16);
     TMR_REQUIRE(W % 8 == 0);
-    constexpr int RPB = TMR_XPACK16_RPB;
+    constexpr int RPB = XPACK16_RPB;
     const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
     const int64_t nseg = (int64_t)S * NCc * tmr_cdiv(H, RPB) * tmr_cdiv(W, XSEG);
     const int64_t nbord = (int64_t)Hp * Wp - (int64_t)H * W;

@@ -272,9 +272,7 @@ constexpr int TRY = 4;  // max tile rows (the LDS slack rows cover it)
 // rows kernel FMA form per template width: scalar v_fma_f32 up to this width
 // (no odd pairs to build; measured k = 3 1.79 vs 2.02 ms, k = 5 2.58 vs 2.65),
 // v_pk_fma_f32 on column pairs above it (k = 15 7.97 vs 10.81 ms; profiles/r02s_*)
-#ifndef TMR_XCORR_SCALAR_MAXW
-#define TMR_XCORR_SCALAR_MAXW 5
-#endif
+constexpr int XCORR_SCALAR_MAXW = 5;
 
 // (a.y, b.x) as ONE v_pk_mov_b32 (left to itself the compiler often builds
 // the odd pair with two v_mov_b32)
@@ -309,7 +307,7 @@ __device__ __forceinline__ void corr_tile(const float *xs, int WS, int lrow0, in
             xe[2 * j] = f32x2{v4[j].x, v4[j].y};
             xe[2 * j + 1] = f32x2{v4[j].z, v4[j].w};
         }
-        if constexpr (KW <= TMR_XCORR_SCALAR_MAXW) {
+        if constexpr (KW <= XCORR_SCALAR_MAXW) {
         // scalar v_fma_f32 on the even-pair registers' halves: no odd pairs
 #pragma unroll
         for (int r = 0; r < TRY; ++r) {
@@ -520,15 +518,8 @@ constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
 // leaves the L2 latency exposed; measured at 128^2 E = 3, config-B mix: PF
 // 1/2/3/4/5/8 = 3.74/4.10/3.61/3.09/4.56/3.24 ms, profiles/r02ad_*, r02ae_*).
 // 3-term kernel: 1 row (PF 2/4: 5.85/5.28 vs 4.67 ms).
-#ifndef TMR_XCORR_PF1
-#define TMR_XCORR_PF1 4
-#endif
-#ifndef TMR_XCORR_PF3_WIDE  // 3-term, >= 6 tiles per wave (W >= 192, LDS-bound occupancy): 3 rows (r03t)
-#define TMR_XCORR_PF3_WIDE 3
-#endif
-#ifndef TMR_XCORR_PF3
-#define TMR_XCORR_PF3 1
-#endif
+// 3-term, >= 6 tiles per wave (W >= 192, LDS-bound occupancy): 3 rows (r03t).
+constexpr int XCORR_PF1 = 4, XCORR_PF3 = 1, XCORR_PF3_WIDE = 3;
 constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -677,7 +668,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int PF = SPLIT ? (NTW >= 6 ? TMR_XCORR_PF3_WIDE : TMR_XCORR_PF3) : TMR_XCORR_PF1;  // (rows)
+    constexpr int PF = SPLIT ? (NTW >= 6 ? XCORR_PF3_WIDE : XCORR_PF3) : XCORR_PF1;  // (rows)
     V ah[PF][NK], al[PF][NK];
     auto afrag = [&](int i, int nk, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);

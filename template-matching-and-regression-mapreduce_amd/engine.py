@@ -3,10 +3,11 @@
 ``TMREngine`` runs, for a batch of B images x E exemplars (U = B*E matching
 units), everything after the frozen backbone on libtmr.so:
 
-  upsample x2 + input_proj       tmr_upsample_proj   matching_net.py:50-56
+  input_proj (+ upsample x2)     tmr_split_conv_store + tmr_upsample2x   matching_net.py:50-56
   exemplar templates             tmr_templates       template_matching.py:55-76
-  depthwise xcorr + pad + scale  tmr_xcorr           template_matching.py:23-41,97
-  decoders + heads (fused)       tmr_conv_heads      regression_head.py, matching_net.py:63-75
+  depthwise xcorr + pad + scale  tmr_xcorr_out       template_matching.py:23-41,97
+  decoders + heads (fused)       tmr_split_conv_heads + tmr_heads_reduce
+                                                     regression_head.py, matching_net.py:63-75
   peaks + decode                 tmr_peaks_decode    TM_utils.py:224-305
   NMS over the exemplar union    tmr_nms             TM_utils.py:307-323, demo.py:106-130
 
@@ -106,10 +107,17 @@ _COST_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "xcorr_cos
 
 
 def _load_xcorr_cost(path: str = _COST_JSON):
+    """The rocprof-swept per-k cost table (xcorr_cost.json).  Missing file:
+    None (the built-in tables above apply).  A file that exists but does not
+    parse raises: a silently moved crossover would change which
+    kernel runs."""
     if not os.path.exists(path):
         return None
-    with open(path) as fh:
-        d = json.load(fh)
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except ValueError as err:
+        raise TMRError(f"{path}: malformed correlation cost table ({err})") from err
     reg = d.get("regimes", {})
 
     def per_unit(name, algo, area):
@@ -123,8 +131,8 @@ def _load_xcorr_cost(path: str = _COST_JSON):
             "mfma": (per_unit("r128_e3_fp32", "mfma", 1.0), per_unit("r192_e16_fp32", "mfma", 2.25)),
             "mfma1": (per_unit("r128_e3_bf16", "mfma", 1.0), per_unit("r192_e16_bf16", "mfma", 2.25)),
         }
-    except (KeyError, ValueError):
-        return None
+    except (KeyError, ValueError, TypeError) as err:
+        raise TMRError(f"{path}: correlation cost table lacks a regime or algorithm ({err!r})") from err
     return table, d.get("source", path)
 
 
@@ -181,33 +189,6 @@ class _PackCache:
         val = build()
         self._d[name] = (key, tuple(weakref.ref(t) for t in tensors), val)
         return val
-
-
-def pack_conv(w: torch.Tensor) -> torch.Tensor:
-    """[N,C,ks,ks] fp32 -> tmr_conv_pack layout (include/tmr.h)."""
-    require_gpu(w, "conv weight")
-    w = w.detach().float().contiguous()
-    N, C, ks, ks2 = w.shape
-    if ks != ks2:
-        raise TMRError("square kernels only (regression_head.py:7)")
-    n = load().tmr_conv_pack_size(N, C, ks)
-    if n <= 0:
-        raise TMRError(f"unsupported conv shape {tuple(w.shape)}")
-    out = torch.empty(n, device=w.device, dtype=torch.float32)
-    call("tmr_conv_pack", ptr(w), N, C, ks, ptr(out), stream())
-    return out
-
-
-def pack_wino(w: torch.Tensor) -> torch.Tensor:
-    """[N,C,3,3] fp32 -> U = G g G^T in the tmr_wino_pack layout (include/tmr.h)."""
-    require_gpu(w, "conv weight")
-    w = w.detach().float().contiguous()
-    N, C, k1, k2 = w.shape
-    if (k1, k2) != (3, 3):
-        raise TMRError("Winograd F(2x2,3x3) needs 3x3 kernels")
-    out = torch.empty(load().tmr_wino_pack_size(N, C), device=w.device, dtype=torch.float32)
-    call("tmr_wino_pack", ptr(w), N, C, ptr(out), stream())
-    return out
 
 
 def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -320,21 +301,6 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     return out
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool, packed=None):
-    """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the MFMA kernel."""
-    require_gpu(x, "conv input")
-    x = x.float().contiguous()
-    U, C, H, W = x.shape
-    N = w.shape[0]
-    if w.shape[1] != C:
-        raise TMRError(f"conv expects {w.shape[1]} input channels, got {C}")
-    wp = packed if packed is not None else pack_conv(w)
-    out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
-    call("tmr_conv_store", ptr(x), C, None, None, 0, U, H, W, ptr(wp),
-         ptr(b.detach().float().contiguous()), N, w.shape[-1], int(leaky), ptr(out), stream())
-    return out
-
-
 def _h2d(arr: np.ndarray, device, dtype=None) -> torch.Tensor:
     """A small host array on the device WITHOUT a stream sync: staged through
     torch's caching pinned-memory allocator and copied non_blocking (the
@@ -372,10 +338,8 @@ class TMREngine:
         # per image when several exemplars share it (fp32, changes only the
         # summation order; same 1e-5 contract)
         self.share_fp_half = True
-        # decoder conv kernel: "split" = direct implicit GEMM on 16-bit MFMA
-        # (conv_split.hip, cfg.precision), "wino" = Winograd F(2x2,3x3) on
-        # fp32 MFMA, "direct" = implicit GEMM on fp32 MFMA
-        self.decoder_algo = "split"
+        # every conv runs on the split 16-bit-MFMA implicit GEMM
+        # (conv_split.hip) in cfg.precision
         prec_code(cfg.precision)
         # split kernel + fusion: run the decoder's fp half on [up2x(f); 1]
         # with weights folded through input_proj (Cin+1 = 257 instead of 512
@@ -393,9 +357,6 @@ class TMREngine:
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
-        # split path: input_proj at the SAM features' size, then bilinear x2
-        # (the same linear map as input_proj(up2x(f)), 4x fewer MFMAs)
-        self.proj_before_upsample = True
         self._fp_memo = None
         self._acc0_memo = None
         self.last_decoder_flops = 0.0
@@ -411,12 +372,7 @@ class TMREngine:
             out.append((self.P[f"{pre}.layer.{2 * l}.weight"], self.P[f"{pre}.layer.{2 * l}.bias"]))
         return out
 
-    def _proj(self):
-        w, b = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
-        wp = self._cache.get("proj", [w], lambda: pack_conv(w))
-        return wp, b.detach().float().contiguous(), w.shape[0], w.shape[1]
-
-    def _fused_decoders(self, split_c0: int = 0, algo: str = "direct", fold: bool = False):
+    def _fused_decoders(self, split_c0: int = 0, fold: bool = False):
         """Layer-0 weights of decoder_b and decoder_o concatenated along N, with
         the 1x1 heads as a [Npad,5] epilogue matrix (only for 1-layer decoders).
         split_c0 > 0 additionally packs the input-channel halves [:c0] / [c0:]
@@ -453,12 +409,8 @@ class TMREngine:
             hw[n0:n0 + no, 4] = ow.detach().float().reshape(no)
             hb[4] = ob.detach().float().reshape(())
             c0_full = cfg.emb_dim if cfg.fusion else 0
-            if algo == "split":
-                prec = cfg.precision
-                pk = lambda w_, c0: pack_split_w(w_, c0, prec)  # noqa: E731
-            else:
-                pk0 = pack_wino if algo == "wino" else pack_conv
-                pk = lambda w_, c0: pk0(w_)  # noqa: E731
+            prec = cfg.precision
+            pk = lambda w_, c0: pack_split_w(w_, c0, prec)  # noqa: E731
             split = None
             if fold:
                 # fp half folded through input_proj: [N, Cin+1, k, k]; the
@@ -481,8 +433,7 @@ class TMREngine:
             full = None if split_c0 else pk(W, c0_full)
             return full, Bv, N, W.shape[1], hw.contiguous(), hb.contiguous(), split, None
 
-        return self._cache.get(f"fused_dec{split_c0}_{algo}_{cfg.precision}_{int(fold)}", tensors,
-                               build)
+        return self._cache.get(f"fused_dec{split_c0}_{cfg.precision}_{int(fold)}", tensors, build)
 
     def _bias_plane(self, wbias: torch.Tensor, H: int, W: int) -> torch.Tensor:
         """conv'(1) of the folded projection bias (wbias [N,1,k,k]): the
@@ -516,14 +467,10 @@ class TMREngine:
 
     def _conv(self, name: str, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool):
         """One nn.Conv2d (+ LeakyReLU) of the general-depth stack on the
-        engine's decoder kernel."""
-        if self.decoder_algo == "split":
-            prec = self.cfg.precision
-            wp = self._cache.get(f"{name}_split_{prec}", [w],
-                                 lambda: pack_split_w(w, w.shape[1], prec))
-            return conv2d_split(x, w, b, leaky, prec, wp)
-        wp = self._cache.get(name, [w], lambda: pack_conv(w))
-        return conv2d(x, w, b, leaky, wp)
+        split decoder kernel."""
+        prec = self.cfg.precision
+        wp = self._cache.get(f"{name}_split_{prec}", [w], lambda: pack_split_w(w, w.shape[1], prec))
+        return conv2d_split(x, w, b, leaky, prec, wp)
 
     # ------------------------------------------------------------ forward
     def _feat_absmax(self, feats: torch.Tensor) -> torch.Tensor:
@@ -556,60 +503,48 @@ class TMREngine:
         self._absmax_memo = {}
         up = self.cfg.feature_upsample
         H, W = (2 * Hin, 2 * Win) if up else (Hin, Win)
-        if self.decoder_algo == "split":
-            # 1x1 conv on the split kernel from records of up2x(f) packed
-            # straight from the SAM features; f[0] (the module API output,
-            # matching_net.py:81) by the upsample kernel alone.  The fp32-grade
-            # 3-term split except under the bf16 contract, where fp feeds only
-            # one-term bf16 arithmetic downstream (the correlation and the
-            # decoders' f_TM half; the fp half is folded from the features):
-            # one bf16 term here too (forward error measured within 1e-2)
-            pprec = "bf16" if self.cfg.precision == "bf16" else "fp32"
-            pcode = prec_code(pprec)
-            pw, pb = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
-            N, Cw = pw.shape[0], pw.shape[1]
-            if Cw != Cin:
-                raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
-            wp, wmax = self._cache.get(f"proj_split_{pprec}", [pw], lambda: pack_split_w(pw, Cin, pprec))
-            xmax = self._feat_absmax(feats)
-            # the 1x1 projection commutes with the bilinear x2 (both linear;
-            # the interpolation weights of each output sum to 1, so the bias
-            # passes through): project at the features' size, then upsample
-            # the projection -- a quarter of the MFMA work
-            # (input_proj(up2x(f)) and up2x(input_proj(f)) differ in fp32
-            # rounding only)
-            early = up and self.proj_before_upsample
-            Hq, Wq = (Hin, Win) if early else (H, W)
-            n = load().tmr_split_xpack_size(B, Cin, Hq, Wq, 1, pcode)
-            xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
-            call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, int(up and not early), 0, 1, pcode,
-                 ptr(xmax), ptr(xp), stream())
-            fq = torch.empty((B, N, Hq, Wq), device=feats.device, dtype=torch.float32)
-            call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
-                 ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
-                 0, stream())
-            if early:
-                fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
-                call("tmr_upsample2x", ptr(fq), B * N, Hin, Win, ptr(fp), stream())
-            else:
-                fp = fq
-            f0 = None
-            if want_f0:
-                if up:
-                    f0 = torch.empty((B, Cin, H, W), device=feats.device, dtype=torch.float32)
-                    call("tmr_upsample2x", ptr(feats), B * Cin, Hin, Win, ptr(f0), stream())
-                else:
-                    f0 = feats
-            return fp, f0
-        wp, b, N, Cw = self._proj()
+        # 1x1 conv on the split kernel from records of up2x(f) packed
+        # straight from the SAM features; f[0] (the module API output,
+        # matching_net.py:81) by the upsample kernel alone.  The fp32-grade
+        # 3-term split except under the bf16 contract, where fp feeds only
+        # one-term bf16 arithmetic downstream (the correlation and the
+        # decoders' f_TM half; the fp half is folded from the features):
+        # one bf16 term here too (forward error measured within 1e-2)
+        pprec = "bf16" if self.cfg.precision == "bf16" else "fp32"
+        pcode = prec_code(pprec)
+        pw, pb = self.P["input_proj.0.weight"], self.P["input_proj.0.bias"]
+        N, Cw = pw.shape[0], pw.shape[1]
         if Cw != Cin:
             raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
-        fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
+        wp, wmax = self._cache.get(f"proj_split_{pprec}", [pw], lambda: pack_split_w(pw, Cin, pprec))
+        xmax = self._feat_absmax(feats)
+        # the 1x1 projection commutes with the bilinear x2 (both linear;
+        # the interpolation weights of each output sum to 1, so the bias
+        # passes through): project at the features' size, then upsample
+        # the projection -- a quarter of the MFMA work
+        # (input_proj(up2x(f)) and up2x(input_proj(f)) differ in fp32
+        # rounding only)
+        Hq, Wq = Hin, Win
+        n = load().tmr_split_xpack_size(B, Cin, Hq, Wq, 1, pcode)
+        xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
+        call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, 0, 0, 1, pcode,
+             ptr(xmax), ptr(xp), stream())
+        fq = torch.empty((B, N, Hq, Wq), device=feats.device, dtype=torch.float32)
+        call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
+             ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
+             0, stream())
+        if up:
+            fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
+            call("tmr_upsample2x", ptr(fq), B * N, Hin, Win, ptr(fp), stream())
+        else:
+            fp = fq
         f0 = None
         if want_f0:
-            f0 = torch.empty((B, Cin, H, W), device=feats.device, dtype=torch.float32) if up else feats
-        call("tmr_upsample_proj", ptr(feats), B, Cin, Hin, Win, int(up), ptr(wp), ptr(b), N,
-             ptr(fp), ptr(f0) if (want_f0 and up) else None, stream())
+            if up:
+                f0 = torch.empty((B, Cin, H, W), device=feats.device, dtype=torch.float32)
+                call("tmr_upsample2x", ptr(feats), B * Cin, Hin, Win, ptr(f0), stream())
+            else:
+                f0 = feats
         return fp, f0
 
     def match(self, fp: torch.Tensor, unit_image: Sequence[int], unit_boxes: np.ndarray,
@@ -674,7 +609,9 @@ class TMREngine:
         # the minimum DRAM traffic of this launch: the kernels stage each
         # image's fp plane once for all its units (read once per IMAGE), and
         # write one f_TM plane per unit
-        self.last_xcorr_dram_bytes = 4.0 * C * H * W * (len(set(int(i) for i in unit_image)) + U)
+        # (fp32 reads; the f_TM write is bf16, 2 B, under out16)
+        nimg = len(set(int(i) for i in unit_image))
+        self.last_xcorr_dram_bytes = float(C * H * W) * (4.0 * nimg + (2.0 if out16 else 4.0) * U)
         self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 
@@ -693,26 +630,21 @@ class TMREngine:
             # share the fp half of the decoder conv across an image's exemplars
             # when that removes work (U >= 2B): conv_fp once per image, then
             # the per-unit kernel starts from it and runs only the f_TM half
-            algo = self.decoder_algo
-            fold0 = algo == "split" and cfg.fusion and self.fold_proj and feats is not None
+            fold0 = cfg.fusion and self.fold_proj and feats is not None
             # module API (reuse_image_work): the reference's callers run one
             # forward per exemplar on the SAME image features (demo.py:111,
             # trainer.py:96); the image's fp half is then computed once and
             # kept for the next calls (_acc0_memo)
             share = self.share_fp_half and cfg.fusion and (U >= 2 * B or (self.reuse_image_work and fold0))
-            if algo == "wino" and cfg.decoder_kernel_size != 3:
-                algo = "direct"
-            wino, splitk = algo == "wino", algo == "split"
             # the bf16 contract keeps the per-image fp half (acc0) in bf16:
             # half the heads launch's initial-value read (a chip-wide burst
             # before the first MFMA: 12% of the one-term kernel, r02ah;
             # measured 10.49 -> 10.07 ms per 48 units, r02ak).  Not under
             # "f16" (its 1e-3 contract: b 1.8e-3 with a bf16 acc0, r02ak).
-            acc16 = splitk and share and cfg.precision == "bf16"
+            acc16 = share and cfg.precision == "bf16"
             ks = cfg.decoder_kernel_size
-            fold = splitk and cfg.fusion and self.fold_proj and feats is not None
-            wp, bias, N, Cw, hw, hb, split, wbias = self._fused_decoders(C0 if share else 0, algo,
-                                                                          fold)
+            fold = fold0
+            wp, bias, N, Cw, hw, hb, split, wbias = self._fused_decoders(C0 if share else 0, fold)
             if Cw != C0 + C1:
                 raise TMRError(f"decoders expect {Cw} input channels, got {C0 + C1}")
             bplane = None
@@ -746,7 +678,7 @@ class TMREngine:
                                         ones=False)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
-            elif splitk:
+            else:
                 # 16-bit operand records; one activation scale per conv launch
                 # (both sources of a virtual concat share it); bf16 records
                 # are unscaled (no reductions; f_TM may be a bf16 plane)
@@ -762,7 +694,7 @@ class TMREngine:
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
             if share:
                 wp_fp, wp_tm, zero_b = split
-                if splitk and acc0 is None:  # acc0 in the kernel's tiled accumulator layout (private)
+                if acc0 is None:  # acc0 in the kernel's tiled accumulator layout (private)
                     acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
                                        dtype=torch.float32)
                     fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0)
@@ -773,53 +705,31 @@ class TMREngine:
                          ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
                     if fold and self.reuse_image_work:
                         self._acc0_store(feats, split, H, W, acc0)
-                elif splitk:
-                    pass  # the image's cached fp half
-                else:
-                    acc0 = torch.empty((B, N, H, W), device=dev, dtype=torch.float32)
-                if splitk:
-                    pass  # launched above
-                elif wino:
-                    call("tmr_wino_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
-                         ptr(zero_b), N, 0, None, ptr(acc0), stream())
-                else:
-                    call("tmr_conv_store", ptr(fp), C0, None, None, 0, B, H, W, ptr(wp_fp),
-                         ptr(zero_b), N, ks, 0, ptr(acc0), stream())
+                # else: the image's cached fp half
                 wp, src0, C0k = wp_tm, None, 0
             ev = None
             if self.decoder_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            s0 = ptr(src0) if src0 is not None else None
             a0 = ptr(acc0) if acc0 is not None else None
             fl = (SPLIT_TILED_INIT | (SPLIT_INIT_BF16 if acc16 else 0)) if a0 is not None else 0
             if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
                 a0 = ptr(bplane)
                 fl = SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
-            if splitk:
-                call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
-                     U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
-                     a0, ptr(part), fl, stream())
-            elif wino:
-                call("tmr_wino_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
-                     ptr(bias), N, 1, ptr(hw), a0, ptr(part), stream())
-            else:
-                call("tmr_conv_heads", s0, C0k, ptr(ui), ptr(f_tm), C1, U, H, W, ptr(wp),
-                     ptr(bias), N, ks, 1, ptr(hw), a0, ptr(part), stream())
+            call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
+                 U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
+                 a0, ptr(part), fl, stream())
             if ev is not None:
                 ev[1].record()
                 self.decoder_events.append(ev)
-            if wino:  # executed: 16 transform-domain GEMMs over 2x2 tiles
-                tiles = ((H + 1) // 2) * ((W + 1) // 2)
-                self.last_decoder_flops = 2.0 * 16 * tiles * N * (C0k + C1) * U
-                self.last_shared_flops = 2.0 * 16 * tiles * N * C0 * B if share else 0.0
-            else:  # direct conv (the split kernel executes 3 16-bit MFMA terms per product)
-                self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * ks ** 2 * U
-                self.last_shared_flops = 2.0 * H * W * N * C0 * ks ** 2 * B if share else 0.0
-            self.last_decoder_algo = algo
+            # direct conv FLOPs (the kernel executes 3 16-bit MFMA terms per
+            # product under the fp32 contract)
+            self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * ks ** 2 * U
+            self.last_shared_flops = 2.0 * H * W * N * C0 * ks ** 2 * B if share else 0.0
+            self.last_decoder_algo = "split"
             o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
             b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
-            call("tmr_heads_reduce", ptr(part), N, 64 if wino else 128, U, H, W, ptr(hb), ptr(o),
+            call("tmr_heads_reduce", ptr(part), N, 128, U, H, W, ptr(hb), ptr(o),
                  ptr(b) if b is not None else None, stream())
             return o, b
         # general depth: per-decoder conv stack, heads as 1x1 convs
@@ -862,10 +772,9 @@ class TMREngine:
         # version AND identity (as _PackCache), and the path options that
         # change the projection's arithmetic
         params = (self.P["input_proj.0.weight"], self.P["input_proj.0.bias"])
-        pkey = (_version_key(params), self.cfg.precision, self.proj_before_upsample,
-                self.cfg.feature_upsample)
+        pkey = (_version_key(params), self.cfg.precision, self.cfg.feature_upsample)
         if self.reuse_image_work and self._same_image(m, feats) and m[3] == pkey and \
-                all(r() is t for r, t in zip(m[5], params)) and self.decoder_algo == "split":
+                all(r() is t for r, t in zip(m[5], params)):
             fp, f0 = m[4], None
             if want_aux:  # f[0]: a fresh tensor per call, like the reference's
                 f0 = feats
@@ -886,7 +795,7 @@ class TMREngine:
         else:
             # a bf16 f_TM plane only where the decode packs it into bf16
             # records and nothing else reads it
-            split1 = self.decoder_algo == "split" and self.cfg.decoder_num_layer == 1
+            split1 = self.cfg.decoder_num_layer == 1
             f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux,
                                     allow_bf16=split1 and not want_aux)
         o, b = self.decode(fp, f_tm, unit_image, feats)

@@ -5,16 +5,16 @@ Same constructors, reference initialisation (N(0, 0.01) weights, zero bias,
 :17-24) and state_dict keys (``layer.<2i>.weight``, ``head.0.weight``).
 ``Decoder_model`` runs on the split 16-bit-MFMA implicit-GEMM kernel
 (tmr_split_conv_store; ``precision`` "fp32" = 3-term fp16 split, the fp32
-1e-5 contract; "bf16" = config C), the 1x1 heads on the fp32 MFMA kernel
-(tmr_conv_store).  Inside
-``matching_net`` the decoders and heads are not called one by one: the
-fused kernel (tmr_conv_heads) consumes their parameters directly.
+1e-5 contract; "bf16" = config C), the 1x1 heads on the same kernel at
+ks = 1 (3-term split, fp32 contract).  Inside ``matching_net`` the decoders
+and heads are not called one by one: the fused kernel (tmr_split_conv_heads)
+consumes their parameters directly.
 """
 from __future__ import annotations
 
 from torch import nn
 
-from .engine import conv2d, conv2d_split
+from .engine import conv2d_split
 
 
 class Decoder_model(nn.Module):
@@ -56,7 +56,7 @@ class _Head1x1(nn.Module):
 
     def forward(self, x):
         conv = self.head[0]
-        return conv2d(x, conv.weight, conv.bias, leaky=False)
+        return conv2d_split(x, conv.weight, conv.bias, False, "fp32")
 
     def reset_parameters(self):
         for module in self.modules():

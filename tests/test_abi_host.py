@@ -40,9 +40,6 @@ def test_struct_layouts():
 
 def test_size_queries_no_gpu():
     L = tmr_amd.load()
-    assert L.tmr_conv_pack_size(2048, 1024, 3) == 16 * 128 * 9 * 8 * 128
-    assert L.tmr_conv_pack_size(512, 256, 1) == 4 * 8 * 32 * 128
-    assert L.tmr_conv_pack_size(10, 10, 4) == -1
     assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
     assert L.tmr_nms_work_size(10, 4, 5, 3) > 10 * 40
     # bounded: the IoU words of 64 images x 49,152 candidates stay within the strip budget
@@ -68,7 +65,11 @@ def test_split_size_queries_no_gpu():
 
 def test_invalid_arguments_return_codes():
     L = tmr_amd.load()
-    assert L.tmr_conv_pack(None, 1, 1, 3, None, None) == -1
+    assert L.tmr_heads_reduce(None, 8, 128, 1, 4, 4, None, None, None, None) == -1
+    assert L.tmr_upsample2x(None, 1, 4, 4, None, None) == -1
+    # the compact reference-exp table: a malformed blob is refused
+    junk = np.zeros(64, np.uint8)
+    assert L.tmr_exp_table_decode(junk.ctypes.data, junk.size, None, 0) == -1
     assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None,
                        None) == -1
     assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0, 0.5, *([None] * 7)) == -1
@@ -255,3 +256,31 @@ def test_template_matching_members():
     assert m._native()
     m.matching_algorithm = lambda f, t: f
     assert not m._native()  # a replaced member routes through the reference loop
+
+
+def test_xcorr_cost_table_committed_crossovers(tmp_path):
+    """the live correlation cost model is the committed rocprof
+    sweep (xcorr_cost.json), with the crossovers DESIGN.md §4.3 documents
+    (single-size launches: 128^2 E=3 fp32 from k=11, one-term from k=5;
+    192^2 E=16 fp32 from k=7, one-term from k=5); a malformed or incomplete
+    table raises instead of silently moving them."""
+    import json
+    from tmr_amd import engine as e
+    assert "xcorr_crossover.json" in e.XCORR_COST_SOURCE
+
+    def first_mfma(upi, one):
+        return min(k for k in range(1, 32, 2)
+                   if e.xcorr_choice(np.full(8, k), np.full(8, k), upi, True, one) == "mfma")
+    assert first_mfma(3, False) == 11 and first_mfma(3, True) == 5
+    assert first_mfma(16, False) == 7 and first_mfma(16, True) == 5
+    bad = tmp_path / "bad.json"
+    bad.write_text("{not json")
+    with pytest.raises(tmr_amd.TMRError, match="malformed"):
+        e._load_xcorr_cost(str(bad))
+    d = json.load(open(e._COST_JSON))
+    d["regimes"].pop("r192_e16_bf16")
+    part = tmp_path / "part.json"
+    part.write_text(json.dumps(d))
+    with pytest.raises(tmr_amd.TMRError, match="lacks"):
+        e._load_xcorr_cost(str(part))
+    assert e._load_xcorr_cost(str(tmp_path / "absent.json")) is None

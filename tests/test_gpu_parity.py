@@ -181,30 +181,6 @@ def test_decoder_conv_vs_torch(C, N, H, W, ks):
     assert normwise(got, ref) <= TOL
 
 
-@pytest.mark.parametrize("C,N,H,W,leaky", [(64, 64, 32, 40, True), (40, 72, 17, 33, True),
-                                           (13, 200, 9, 70, False), (1024, 256, 16, 32, True)])
-def test_wino_conv_vs_torch(C, N, H, W, leaky):
-    """Winograd F(2x2,3x3) kernel (tmr_wino_conv_store) vs ATen conv2d, incl.
-    odd sizes, channel counts off the 8/64 granules and an acc_init input."""
-    from tmr_amd._lib import call, ptr, stream
-    from tmr_amd.engine import pack_wino
-    torch.manual_seed(C * 7 + N)
-    x = torch.randn(2, C, H, W)
-    w = torch.randn(N, C, 3, 3) * (1.0 / (3 * C ** 0.5))
-    b = torch.randn(N)
-    init = torch.randn(2, N, H, W)
-    ref = torch.nn.functional.conv2d(x, w, b, padding=1) + init
-    if leaky:
-        ref = torch.nn.functional.leaky_relu(ref, 0.01)
-    out = torch.empty((2, N, H, W), device=DEV)
-    up = pack_wino(cuda(w))
-    xd, bd, initd = cuda(x), cuda(b), cuda(init)  # keep alive across the async launch
-    call("tmr_wino_conv_store", ptr(xd), C, None, None, 0, 2, H, W, ptr(up), ptr(bd), N,
-         int(leaky), ptr(initd), ptr(out), stream())
-    torch.cuda.synchronize()
-    assert normwise(out.cpu().numpy(), ref.numpy()) <= TOL
-
-
 SPLIT_TOL = {"fp32": TOL, "f16": 1e-3, "bf16": 1e-2}
 
 
@@ -285,8 +261,7 @@ def test_split_conv_scales_and_two_sources(scale):
 def test_upsample2x_tiled_and_projection_order(Hin, Win):
     """tmr_upsample2x (LDS-tiled, 32x128 output tiles) bit-exact against the C
     restatement at tile-edge and W % 4 != 0 sizes; the engine's projection
-    input_proj at the features' size then up2x (default) and input_proj on
-    up2x(f) (proj_before_upsample=False) both within the fp32 contract of
+    (input_proj at the features' size, then up2x) within the fp32 contract of
     ATen's conv2d(interpolate(f)) (matching_net.py:50-51,56)."""
     from tmr_amd._lib import call, ptr, stream
     torch.manual_seed(Hin * 100 + Win)
@@ -301,11 +276,9 @@ def test_upsample2x_tiled_and_projection_order(Hin, Win):
     ref = torch.nn.functional.conv2d(
         torch.nn.functional.interpolate(f, scale_factor=2, mode="bilinear", align_corners=False),
         P["input_proj.0.weight"], P["input_proj.0.bias"])
-    for early in (True, False):
-        eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=40))
-        eng.proj_before_upsample = early
-        fp, _ = eng.project(fd)
-        assert normwise(fp.cpu().numpy(), ref.numpy()) <= TOL, early
+    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=40))
+    fp, _ = eng.project(fd)
+    assert normwise(fp.cpu().numpy(), ref.numpy()) <= TOL
 
 
 def _xrecords_ref(x, ks, prec, xmax):
@@ -422,24 +395,32 @@ def test_split_acc_slab_bf16():
              ptr(zero), N, 0, None, ptr(out), SPLIT_OUT_BF16, stream())
 
 
-def test_wino_matches_direct_decoders():
+def test_shared_and_unshared_fp_half_agree():
+    """The decoder's fp half computed once per image (acc0 shared by the
+    image's exemplars) and per unit in the same launch give the same maps
+    within the fp32 contract, folded and unfolded projection both, and
+    both match the oracle forward."""
     B, E = 2, 2
     P = synth.reference_state_dict(4, cin=64, emb=96, obj_bias=-0.3)
-    feats = cuda(synth.sam_features(18, B, 64, 20, 23))
+    feats_h = synth.sam_features(18, B, 64, 20, 23)
+    feats = cuda(feats_h)
     ex, _ = synth.exemplar_set(19, B, E, 40, 46, 3, 9)
     ui = np.repeat(np.arange(B), E)
     res = {}
-    for algo in ("split", "wino", "direct"):
+    for fold in (True, False):
         for share in (True, False):
             eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=96))
-            eng.decoder_algo, eng.share_fp_half = algo, share
+            eng.fold_proj, eng.share_fp_half = fold, share
             r = eng.forward_units(feats, ui, ex.reshape(-1, 4))
-            assert eng.last_decoder_algo == algo
-            res[(algo, share)] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
-    ref = res[("direct", False)]
-    for k, (o, b) in res.items():
-        assert normwise(o, ref[0]) <= TOL, k
-        assert normwise(b, ref[1]) <= TOL, k
+            assert eng.last_decoder_algo == "split"
+            assert (eng.last_shared_flops > 0) == share
+            res[(fold, share)] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
+    for u in range(B * E):
+        ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats_h[ui[u]:ui[u] + 1]),
+                                            [torch.from_numpy(ex.reshape(-1, 4)[u:u + 1])], P)
+        for k, (o, b) in res.items():
+            assert normwise(o[u], ro[0][0].numpy()) <= TOL, (k, u)
+            assert normwise(b[u], rb[0][0].numpy()) <= TOL, (k, u)
 
 
 def test_heads_vs_torch():

@@ -391,15 +391,28 @@ def test_tar_reads_do_not_rescan_headers(tmp_path, monkeypatch):
         shutil.copyfileobj(fi, fo)
     plain, members = mr.tar_members(str(gz / "Easy_0.tar"))
     assert not plain
-    import threading
-    tls = threading.local()
+    tls = mr.TarHandles()
     opened.clear()
     got = [mr.read_member(str(gz / "Easy_0.tar"), m, plain, tls) for m in members]
-    assert len(opened) == 1
+    assert len(opened) == 1 and len(tls) == 1
     want = [b for (p, _, _, _), b in zip(src.items, plain_bytes) if p.endswith("Easy_0.tar")]
     decodable = {m.name for p, m, _, _ in src.items if p.endswith("Easy_0.tar")}
     assert [g for g, m in zip(got, members) if m.name in decodable] == want
-    tls.tf.close()
+    # every handle is released by close(); the next read reopens
+    handle = tls.get(str(gz / "Easy_0.tar"))
+    tls.close()
+    assert len(tls) == 0 and handle.closed
+    assert mr.read_member(str(gz / "Easy_0.tar"), members[0], plain, tls) == got[0]
+    tls.close()
+    # a source over the gzip shard holds no handle after its scan, and close()
+    # releases the readers' handles
+    src2 = mr.TarImageSource(str(gz), ["Easy_0.tar"], _PoolBackbone(), torch.device("cpu"), 2, 3, 5, 0,
+                             input_shape=(32, 32))
+    assert len(src2._tls) == 0
+    src2([0])
+    assert len(src2._tls) >= 1
+    src2.close()
+    assert len(src2._tls) == 0
 
 
 def test_tar_source_feature_cache_roundtrip(tmp_path):
@@ -412,7 +425,7 @@ def test_tar_source_feature_cache_roundtrip(tmp_path):
     src = mr.TarImageSource(str(tmp_path / "tars"), shards, bb, torch.device("cpu"), 2, 3, 5, 0,
                             write_root=str(tmp_path / "feat"), workers=2, input_shape=(128, 128))
     rec = mr.run_mapper(shards, src.counts, 0, 1, src, _cpu_stats, None, batch=3)
-    src.flush()
+    src.close()
     back = mr.NpyFeatureSource(str(tmp_path / "feat"), shards, torch.device("cpu"), 2, 3, 5, 0)
     assert back.counts == src.counts
     assert sorted(back.keys) == sorted(src.keys)
