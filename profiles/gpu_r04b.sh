@@ -21,3 +21,12 @@ for l in sys.stdin:
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/r04b/bench_B.json 2> gpurun_out/r04b/bench_B.err || exit 1
 timeout -k 10 300 python bench.py --config E --no-cpu-baseline > gpurun_out/r04b/bench_E.json 2> gpurun_out/r04b/bench_E.err || exit 1
 for c in B E; do python -c "import json;d=json.load(open('gpurun_out/r04b/bench_$c.json'));print('$c',d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'],d['roofline']['frac'],d['roofline_xcorr']['avg_launch_ms'])"; done
+# heads-kernel timing-only variants (profiles/heads_variants.py; wrong results by design)
+for v in base nobar nowait noacc0 noepi nodma; do
+  if [ $v = base ]; then VAR=""; else VAR=$v; fi
+  TMR_LIB_VARIANT=$VAR timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-xcorr-classes > gpurun_out/r04b/var_$v.json 2> gpurun_out/r04b/var_$v.err || { echo "variant $v failed"; tail -3 gpurun_out/r04b/var_$v.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/r04b/var_$v.json'));print('$v heads ms',d['roofline']['avg_launch_ms'],'step',d['ms_per_step'])"
+done
+timeout -k 10 300 python bench.py --config A --no-cpu-baseline > gpurun_out/r04b/bench_A.json 2> gpurun_out/r04b/bench_A.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04b/prof_A -o run -- python bench.py --config A --steps 20 --no-cpu-baseline --no-xcorr-classes > gpurun_out/r04b/prof_A.log 2>&1 || exit 1
+python -c "import json;d=json.load(open('gpurun_out/r04b/bench_A.json'));print('A',d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'])"

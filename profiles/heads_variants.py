@@ -1,0 +1,104 @@
+"""Timing-only variants of the decoder heads kernel: where
+does the ~16% of the launch that is not MFMA issue go?
+
+Each variant is conv_split.hip with ONE part of the kernel removed by a text
+substitution in a scratch copy of csrc/ (the committed kernel is untouched),
+built as tmr_amd/libtmr_<variant>.so and selected with TMR_LIB_VARIANT by
+bench.py.  Their results are WRONG by construction (no parity) -- only the
+heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
+
+  nobar    no s_barrier at the end of each barrier step (LDS reuse races)
+  nowait   no counted vmcnt wait before those barriers (DMA not awaited)
+  noacc0   no initial-value (acc0) read: accumulators start at zero
+  noepi    no heads epilogue: one dummy store per block
+  nodma    no LDS-DMA at all (halo and weights never loaded)
+
+    python profiles/heads_variants.py build [variants...]   # here, on the CPU
+    python profiles/heads_variants.py clean
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "template-matching-and-regression-mapreduce_amd")
+CSRC = os.path.join(PKG, "csrc")
+
+STEP_BARRIER = """                    wait_vmcnt(G::allowed(sg, part, HALVES));
+                __builtin_amdgcn_s_barrier();"""
+EPI_START = "    // ---------------- epilogue ----------------\n"
+
+
+def _sub(src: str, old: str, new: str, count: int = 1) -> str:
+    n = src.count(old)
+    if n != count:
+        raise SystemExit(f"variant substitution: expected {count} match(es), found {n}: {old[:60]!r}")
+    return src.replace(old, new)
+
+
+def variant_source(name: str, src: str) -> str:
+    if name == "nobar":
+        return _sub(src, STEP_BARRIER, "                    wait_vmcnt(G::allowed(sg, part, HALVES));\n")
+    if name == "nowait":
+        src = _sub(src, """                if constexpr (D == 1)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else
+                    wait_vmcnt(G::allowed(sg, part, HALVES));""", "")
+        return src
+    if name == "noacc0":
+        return _sub(src, "    if (a.acc_init && (a.flags & TMR_SPLIT_TILED_INIT) && (a.flags & TMR_SPLIT_INIT_BF16)) {",
+                    "    if (false) {")
+    if name == "noepi":
+        return _sub(src, EPI_START, EPI_START + """    if constexpr (EPI == 1) {
+        float s_ = 0.0f;
+#pragma unroll
+        for (int in = 0; in < NIN; ++in)
+#pragma unroll
+            for (int jp = 0; jp < 8; ++jp) s_ += acc[in][jp][0];
+        if (s_ == 1234.5f) a.partials[tid] = s_;  // keeps the main loop alive
+        return;
+    }
+""")
+    if name == "nodma":
+        return _sub(src, "    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);",
+                    "    (void)r; (void)dst; (void)voff; (void)soff;")
+    raise SystemExit(f"unknown variant {name}")
+
+
+VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma"]
+
+
+def build(names):
+    for name in names:
+        scratch = os.path.join(PKG, f"build_var_{name}")
+        src_dir = os.path.join(scratch, "csrc")
+        shutil.rmtree(scratch, ignore_errors=True)
+        shutil.copytree(CSRC, src_dir)
+        # the scratch csrc sits one level deeper: point its include path at the repo
+        for f in os.listdir(src_dir):
+            if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile":
+                p = os.path.join(src_dir, f)
+                txt = open(p).read().replace("../../include/", "../../../include/")
+                if f == "conv_split.hip":
+                    txt = variant_source(name, txt)
+                with open(p, "w") as fh:
+                    fh.write(txt)
+        out = os.path.join(PKG, f"libtmr_{name}.so")
+        subprocess.check_call(["make", "-s", "-j8", "-C", src_dir, f"OUT={out}", f"OBJDIR={scratch}/obj"])
+        shutil.rmtree(scratch, ignore_errors=True)
+        print("built", out)
+
+
+def clean():
+    for name in VARIANTS:
+        p = os.path.join(PKG, f"libtmr_{name}.so")
+        if os.path.exists(p):
+            os.remove(p)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "clean":
+        clean()
+    else:
+        build(sys.argv[2:] or VARIANTS)
