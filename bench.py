@@ -430,10 +430,9 @@ def main():
         why_opts = "the run changes the config's options (--batch, --precision, ...)"
         pmc_heads, why_heads = load_pmc(a.config, "heads") if own_options else (None, why_opts)
         pmc_xc, why_xc = load_pmc(a.config, "xcorr") if own_options else (None, why_opts)
-        if pmc_xc and pmc_xc.get("kernel_names") and not all(
-                any(("rows" if k == "valu" else "mfma") in n for n in pmc_xc["kernel_names"])
-                for k in eng.last_xcorr_algo.split("+")):
-            pmc_xc, why_xc = None, "the PMC run measured another correlation kernel"
+        if pmc_xc and pmc_xc.get("kernel_names") and not any(
+                ("rows" if eng.last_xcorr_algo == "valu" else "mfma") in n for n in pmc_xc["kernel_names"]):
+            pmc_xc, why_xc = None, "the PMC run measured the other correlation kernel"
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
@@ -478,17 +477,16 @@ def main():
         # templates, VALU-bound for k >= 11; both fractions, algorithmic work
         xs = float(np.mean(xc_ms)) / 1e3
         xk = eng.last_xcorr_algo
-        kdesc = {"mfma": "MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
-                         + ("v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if prec == "fp32" else
-                            "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
-                                                                       else ("f16", "scaled fp16"))),
-                 "valu": "VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)"}
         out["roofline_xcorr"] = {
-            "kernel": ("tmr_xcorr_out " + " + ".join(kdesc[k] for k in xk.split("+"))
-                       + " + /hw + pad + scale + max|f_TM|; kernel chosen per template-size class by the "
-                         "measured per-k cost model (engine.XCORR_COST)"),
+            "kernel": ("tmr_xcorr_prec MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
+                       + ("v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if prec == "fp32" else
+                          "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
+                                                                     else ("f16", "scaled fp16")))
+                       if xk == "mfma" else
+                       "tmr_xcorr_prec VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
+                      + " + /hw + pad + scale + max|f_TM|; kernel chosen by the measured per-k cost model "
+                        "(engine.XCORR_COST)",
             "algo": xk,
-            "launches": [{"k": [g[0], g[1]], "units": g[2], "algo": g[3]} for g in eng.last_xcorr_groups],
             "bound": "hbm" if cfg["kmax"] <= 9 else "valu",
             "avg_launch_ms": round(1e3 * xs, 3),
             "hbm_achieved": round(xc_bytes / xs / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,

@@ -51,11 +51,7 @@ typedef struct tmr_unit {
     int64_t tmpl_offset;   /* float offset of this unit's [C,ht,wt] template      */
     int32_t row_offset;    /* sum of ht over the units before this one (the MFMA  */
                            /* correlation's split-template rows, tmr_template_split) */
-    int32_t out_index;     /* the correlation's output plane of this unit: its    */
-                           /* position in the caller's full unit list (a launch   */
-                           /* over a subset of the units writes their planes of   */
-                           /* the full f_TM tensor); = the array index otherwise, */
-                           /* and always under squeeze (tmr_xcorr*)               */
+    int32_t pad_;
 } tmr_unit_t;
 
 /* Per-unit peak-finder parameters (utils/TM_utils.py:236-278). */

@@ -4,16 +4,18 @@
 set -o pipefail
 mkdir -p gpurun_out/r04b
 export TMPDIR=/tmp
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r04b/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r04b/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/r04b/gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04b/smoke.log 2>&1 || { tail -20 gpurun_out/r04b/smoke.log; exit 1; }
 head -1 gpurun_out/r04b/smoke.log
+fi
 S_B='-;5;7;9;11;5,9;7,11;5,9,13'
 S_E='-;9;11;13;17;9,17;11,19;7,13,19;9,15,21;7,11,15,19,23;5,9,13,17,21,25'
-timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --splits "$S_B" > gpurun_out/r04b/split_B_fp32.jsonl 2>&1 || exit 1
-timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --precision bf16 --splits "$S_B" > gpurun_out/r04b/split_B_bf16.jsonl 2>&1 || exit 1
-timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --images 8 --E 16 --H 192 --kmax 31 --splits "$S_E" > gpurun_out/r04b/split_E_fp32.jsonl 2>&1 || exit 1
-timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --images 8 --E 16 --H 192 --kmax 31 --precision bf16 --splits "$S_E" > gpurun_out/r04b/split_E_bf16.jsonl 2>&1 || exit 1
+timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --splits="$S_B" > gpurun_out/r04b/split_B_fp32.jsonl 2>&1 || exit 1
+timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --precision bf16 --splits="$S_B" > gpurun_out/r04b/split_B_bf16.jsonl 2>&1 || exit 1
+timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --images 8 --E 16 --H 192 --kmax 31 --splits="$S_E" > gpurun_out/r04b/split_E_fp32.jsonl 2>&1 || exit 1
+timeout -k 10 300 python profiles/kbench_xcorr.py --mixed --algos mfma --images 8 --E 16 --H 192 --kmax 31 --precision bf16 --splits="$S_E" > gpurun_out/r04b/split_E_bf16.jsonl 2>&1 || exit 1
 grep -h '"split"' gpurun_out/r04b/split_*.jsonl | python -c "
 import sys,json
 for l in sys.stdin:

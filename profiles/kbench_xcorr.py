@@ -48,9 +48,6 @@ def main():
     ap.add_argument("--kmin", type=int, default=3)
     ap.add_argument("--kmax", type=int, default=15)
     ap.add_argument("--precision", default="fp32", help="MFMA operand precision: fp32 (3-term), bf16, f16")
-    ap.add_argument("--splits", default="",
-                    help="with --mixed: ';'-separated class-boundary lists to try (engine.xcorr_split), "
-                         "e.g. '7,11;9;13,19' ('-' = one launch); algos then = auto per class")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, H = a.images, 512, a.H
@@ -70,14 +67,6 @@ def main():
     for name, boxes, ks in sets:
         flops = float(sum(2.0 * C * (H - k + 1) ** 2 * k * k for k in ks))
         nbytes = 2.0 * 4 * C * H * H * len(ks)
-        for sp in [x for x in a.splits.split(";") if x] if a.mixed else []:
-            eng.xcorr_algo = "auto"
-            eng.xcorr_split = None if sp == "-" else [int(v) for v in sp.split(",")]
-            ms = run(eng, fp, ui, boxes, a.reps)
-            print(json.dumps({"split": sp, "prec": a.precision, "k": name, "images": B, "E": a.E, "H": H,
-                              "ms": round(ms, 4), "groups": eng.last_xcorr_groups,
-                              "hbm_frac": round(nbytes / ms / 1e6 / 8000.0, 4)}), flush=True)
-        eng.xcorr_split = None
         for algo in a.algos.split(","):
             eng.xcorr_algo = algo
             try:

@@ -24,10 +24,10 @@ _lib = None
 
 # ABI structs (must match include/tmr.h)
 UNIT_DTYPE = np.dtype({
-    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset", "row_offset", "out_index"],
+    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset", "row_offset"],
     "formats": [np.int32, np.int32, np.int32, np.int32, (np.float32, 4), (np.int32, 4), np.int64,
-                np.int32, np.int32],
-    "offsets": [0, 4, 8, 12, 16, 32, 48, 56, 60],
+                np.int32],
+    "offsets": [0, 4, 8, 12, 16, 32, 48, 56],
     "itemsize": 64,
 })
 PEAK_DTYPE = np.dtype({

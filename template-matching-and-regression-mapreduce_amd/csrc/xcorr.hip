@@ -193,10 +193,9 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
         const float sc = a.squeeze ? 1.0f : *a.scale;
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;  // correctly rounded reciprocal
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_index);  // output plane (subset launches)
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                              : outp + ((size_t)uo * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
+                              : outp + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         if (!a.squeeze) {  // zero border of this band ((yo, xo) stepped, no per-element division)
             int yo = yb0 + (int)threadIdx.x / W, xo = (int)threadIdx.x % W;
             const int sy = NT / W, sx = NT % W;
@@ -460,10 +459,9 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
         const int Ho = H - h + 1, Wo = W - w + 1;
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;  // correctly rounded reciprocal
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_index);  // output plane (subset launches)
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                              : outp + ((size_t)uo * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
+                              : outp + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
         // 4x4 tiles: one 16-B store per lane row (1 KB per wave row).  2x8
         // tiles (twice the FMAs per scalar tap-row load) measured 5.1 vs 5.5
@@ -826,11 +824,10 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_index);  // output plane (subset launches)
         float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                    : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)uo * a.C + c) * plane)
-                         : outp + ((size_t)uo * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
+                    : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)u * a.C + c) * plane)
+                         : outp + ((size_t)u * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
         const int y = yb0 + tr * 16 + l16;
         if (row_live && y < yb1) {
             const bool vy = y >= ph && y < ph + Ho;

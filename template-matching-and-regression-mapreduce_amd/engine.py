@@ -150,22 +150,6 @@ if _swept is not None:
 XCORR_MFMA_MIX = 0.4
 
 
-def xcorr_groups(k: np.ndarray, split) -> List[np.ndarray]:
-    """Unit indices (ascending, so image-sorted) of each correlation launch:
-    one launch (split None) or one per class k <= split[0] < k <= split[1]
-    ... of the units' template size k = max(ht, wt); empty classes drop out."""
-    k = np.asarray(k)
-    if not split:
-        return [np.arange(k.size)]
-    edges = [0] + sorted(int(e) for e in split) + [1 << 30]
-    out = []
-    for lo, hi in zip(edges[:-1], edges[1:]):
-        idx = np.nonzero((k > lo) & (k <= hi))[0]
-        if idx.size:
-            out.append(idx)
-    return out
-
-
 def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool,
                  one_term: bool = False) -> str:
     """The cheaper correlation kernel ("valu" or "mfma") for a launch over
@@ -366,10 +350,6 @@ class TMREngine:
         # "valu" or "mfma" (csrc/xcorr.hip)
         self.xcorr_algo = "auto"
         self.last_xcorr_algo = None
-        # correlation launches per template-size class: None = one launch;
-        # a list of class upper bounds on max(ht, wt) (xcorr_groups)
-        self.xcorr_split = None
-        self.last_xcorr_groups = []
         # bf16 contract, detect path: the one-term MFMA correlation writes
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
@@ -592,54 +572,32 @@ class TMREngine:
         if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        min_k = int(min(units["ht"].min(), units["wt"].min()))
         # MFMA operand precision: the fp32 path's 3-term split, or one bf16 /
         # fp16 term under the bf16 contract (config C); the VALU kernels are fp32
         pc = prec_code(cfg.precision)
-        one_term = pc != PREC_CODES["fp32"]
-        # one launch per template-size class (xcorr_groups): each launch stages
-        # its bands with its OWN largest halo, so small templates do not run at
-        # the occupancy of the largest one's LDS footprint
-        kk = np.maximum(units["ht"], units["wt"])
-        groups = xcorr_groups(kk, self.xcorr_split) if not cfg.squeeze else [np.arange(U)]
-        plan = []
-        for idx in groups:
-            g_img = np.asarray(unit_image)[idx]
-            g_mh, g_mw = int(units["ht"][idx].max()), int(units["wt"][idx].max())
-            choice = self.xcorr_algo
-            if choice == "auto":  # measured per-k cost model (XCORR_COST)
-                fits = W % 32 == 0 and W <= 256 and g_mh <= 31 and g_mw <= 31 and \
-                    (32 + g_mh // 2 * 2) * W <= 16384
-                choice = xcorr_choice(units["ht"][idx], units["wt"][idx], len(idx) / max(1, len(set(g_img))),
-                                      fits, one_term=one_term)
-            plan.append((idx, g_img, g_mh, g_mw, choice))
-        algos = sorted(set(p_[4] for p_ in plan))
-        self.last_xcorr_algo = "+".join(algos)
-        self.last_xcorr_groups = [(int(kk[p_[0]].min()), int(kk[p_[0]].max()), len(p_[0]), p_[4]) for p_ in plan]
-        out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algos == ["mfma"]
+        choice = self.xcorr_algo
+        if choice == "auto":  # measured per-k cost model (XCORR_COST)
+            fits = W % 32 == 0 and W <= 256 and mh <= 31 and mw <= 31 and (32 + mh // 2 * 2) * W <= 16384
+            choice = xcorr_choice(units["ht"], units["wt"], U / max(1, len(set(unit_image))), fits,
+                                  one_term=pc != PREC_CODES["fp32"])
+        self.last_xcorr_algo = choice
+        algo = XCORR_ALGOS[choice]
+        out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
                  and not cfg.squeeze and not want_relu and W % 8 == 0)
         self.last_xcorr_out16 = out16
         out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
         relu = torch.empty_like(out) if want_relu else None
-        for idx, g_img, g_mh, g_mw, choice in plan:
-            algo = XCORR_ALGOS[choice]
-            if len(plan) == 1:
-                g_units, g_units_d, g_ranges_d = units, units_d, img_units_d
-            else:
-                g_units = host.subset_units(units, idx)
-                g_units_d = _units_to_device(g_units, dev)
-                g_ranges_d = _h2d(np.asarray(host.image_ranges(g_img, B)), dev)
-            Ug = len(idx)
-            min_k = int(min(g_units["ht"].min(), g_units["wt"].min()))
-            tsplit, rows = None, 0
-            if algo != XCORR_ALGOS["valu"] and tfl > 0:
-                # the MFMA correlation's template operands (per (unit, channel) scale)
-                rows = host.tsplit_rows(g_units)
-                tsplit = torch.empty(load().tmr_template_split_size(Ug, C, rows), device=dev, dtype=torch.uint8)
-                call("tmr_template_split_prec", ptr(tmpl), ptr(g_units_d), Ug, C, rows, pc, ptr(tsplit), stream())
-            call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(g_units_d), ptr(g_ranges_d), Ug, g_mh,
-                 g_mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
-                 ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
-                 rows, algo, min_k, pc, int(out16), stream())
+        tsplit = None
+        if algo != XCORR_ALGOS["valu"] and tfl > 0:
+            # the MFMA correlation's template operands (per (unit, channel) scale)
+            rows = host.tsplit_rows(units)
+            tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
+            call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
+        call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+             mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
+             ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
+             rows if tsplit is not None else 0, algo, min_k, pc, int(out16), stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)

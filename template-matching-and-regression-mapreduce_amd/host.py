@@ -101,22 +101,10 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         units["wt"][u] = wt
         units["tmpl_offset"][u] = off
         units["row_offset"][u] = rows
-        units["out_index"][u] = u
         off += C * ht * wt
         rows += ht * tsplit_nk(wt)
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
     return units, off, max_ht, max_wt
-
-
-def subset_units(units: np.ndarray, idx) -> np.ndarray:
-    """The units `idx` (sorted by image) as one correlation launch's array:
-    tmpl_offset and out_index unchanged (the full template buffer and f_TM
-    tensor), row_offset renumbered for the launch's own tmr_template_split."""
-    sub = units[np.asarray(idx, np.int64)].copy()
-    nk = np.array([tsplit_nk(int(w)) for w in sub["wt"]], np.int64)
-    rows = sub["ht"].astype(np.int64) * nk
-    sub["row_offset"] = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.int32) if len(sub) else rows
-    return sub
 
 
 def image_ranges(unit_image: Sequence[int], B: int) -> np.ndarray:

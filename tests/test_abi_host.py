@@ -284,26 +284,3 @@ def test_xcorr_cost_table_committed_crossovers(tmp_path):
     with pytest.raises(tmr_amd.TMRError, match="lacks"):
         e._load_xcorr_cost(str(part))
     assert e._load_xcorr_cost(str(tmp_path / "absent.json")) is None
-
-
-def test_xcorr_groups_and_subset_units():
-    """Class partition of the correlation launches (engine.xcorr_groups) and a
-    launch's unit subset (host.subset_units): indices ascending (image order
-    kept), every unit in exactly one class, empty classes dropped; the subset
-    keeps tmpl_offset and out_index and renumbers row_offset for its own
-    template split."""
-    from tmr_amd import engine as e
-    k = np.array([3, 15, 7, 9, 31, 5, 11, 3])
-    assert [g.tolist() for g in e.xcorr_groups(k, None)] == [list(range(8))]
-    g = e.xcorr_groups(k, [7, 11, 19])
-    assert [x.tolist() for x in g] == [[0, 2, 5, 7], [3, 6], [1], [4]]
-    assert [x.tolist() for x in e.xcorr_groups(k, [1, 2])] == [list(range(8))]
-    boxes = np.stack([synth.exemplar_box(int(kk), 64, 64, 3, 4) for kk in k])
-    ui = [0, 0, 0, 1, 1, 2, 2, 2]
-    units, tfl, mh, mw = host.build_units(boxes, ui, 64, 64, 16)
-    assert units["out_index"].tolist() == list(range(8))
-    sub = host.subset_units(units, g[0])
-    assert sub["out_index"].tolist() == [0, 2, 5, 7]
-    assert np.array_equal(sub["tmpl_offset"], units["tmpl_offset"][g[0]])
-    assert sub["row_offset"].tolist() == [0, 3, 10, 15]  # ht * nk: 3, 7, 5 (nk 1 up to w 17)
-    assert host.tsplit_rows(sub) == 18

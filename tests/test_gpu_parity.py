@@ -866,44 +866,6 @@ def test_xcorr_mfma_squeeze_and_engine():
                 assert normwise(res[(sq, algo)][u], ref) <= TOL, (sq, algo, u)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("split", [[7], [5, 11], [3, 9, 19], [1, 31]])
-def test_xcorr_grouped_launches(split, prec):
-    """engine.xcorr_split: one correlation launch per template-size class,
-    each over a subset of the units writing its planes of the full f_TM
-    (tmr_unit_t.out_index).  Forced VALU: bit-identical to the single launch;
-    forced MFMA and auto: every unit within its contract of the oracle; every
-    unit's plane written exactly once (none left unwritten); empty classes
-    skipped."""
-    C, H, W, B, E = 8, 96, 96, 3, 6
-    f = synth.normal(31, (B, C, H, W)) * 1.3
-    ks = [1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 23, 31, 29, 5, 21, 25, 3, 27]
-    boxes = np.stack([synth.exemplar_box(k, H, W, (7 * i) % (H - k + 1), (5 * i) % (W - k + 1))
-                      for i, k in enumerate(ks[:B * E])])
-    ui = np.repeat(np.arange(B), E)
-    P = {"matcher.scale": torch.tensor([0.75], device=DEV)}
-    fd = cuda(f)
-    tol = TOL if prec == "fp32" else XCORR_ONE_TERM_TOL[prec]
-    for algo in ("valu", "mfma", "auto"):
-        res = {}
-        for sp in (None, split):
-            eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C, precision=prec))
-            eng.xcorr_algo, eng.xcorr_split = algo, sp
-            out, relu = eng.match(fd, ui, boxes, want_relu=True)
-            res[sp is None] = out.cpu().numpy()
-            assert np.array_equal(relu.cpu().numpy(), np.maximum(res[sp is None], 0))
-            if sp is not None:
-                groups = eng.last_xcorr_groups
-                assert sum(g[2] for g in groups) == B * E and len(groups) >= 1
-        if algo == "valu":
-            assert bits_equal(res[True], res[False])
-        for u in range(B * E):
-            roi, ht, wt = oracle.template_size(boxes[u], H, W)
-            t = oracle.roi_align(f[ui[u]], roi, ht, wt)
-            ref = oracle.xcorr(f[ui[u]], t, 0.75)
-            assert normwise(res[False][u], ref) <= (TOL if algo == "valu" else tol), (algo, u)
-
-
 def test_nms_worst_case_dense_candidates():
     """SURVEY.md §7.3.3 worst case: a centre-only adaptive kernel (exemplars
     under 2 px) with p ~ 0.5 everywhere at cls 0.1 makes EVERY pixel a
