@@ -12,6 +12,9 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
   noacc0   no initial-value (acc0) read: accumulators start at zero
   noepi    no heads epilogue: one dummy store per block
   nodma    no LDS-DMA at all (halo and weights never loaded)
+  l2dma    every DMA re-reads the first chunk's halo / first step's weights:
+           the same instruction stream with real operand data, but L2-resident
+           (no MALL / HBM traffic)
 
     python profiles/heads_variants.py build [variants...]   # here, on the CPU
     python profiles/heads_variants.py clean
@@ -63,10 +66,18 @@ def variant_source(name: str, src: str) -> str:
     if name == "nodma":
         return _sub(src, "    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);",
                     "    (void)r; (void)dst; (void)voff; (void)soff;")
+    if name == "l2dma":
+        src = _sub(src, "        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;",
+                   "        const uint32_t soff = 0u * (uint32_t)(s0 ? hc : hc - h0) * cstride;")
+        src = _sub(src, "buffer_lds16(wr, (lds_ptr_t)w_dst(g, ipt, m), wlane, w_src(g, ipt, m));",
+                   "buffer_lds16(wr, (lds_ptr_t)w_dst(g, ipt, m), wlane, w_src(0, ipt, m));")
+        src = _sub(src, "const uint32_t src = (uint32_t)(sgx * G::tps(px) + tl) * tapstride + (uint32_t)cx * a.Npad * WREC + wnt +",
+                   "const uint32_t src = (uint32_t)tl * tapstride + wnt +")
+        return src
     raise SystemExit(f"unknown variant {name}")
 
 
-VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma"]
+VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma", "l2dma"]
 
 
 def build(names):

@@ -771,24 +771,35 @@ inline int pad_h(int H, int ks) { return (int)tmr_cdiv(H, TH) * TH + ks - 1; }
 inline int pad_w(int W, int ks) { return (int)tmr_cdiv(W, TW) * TW + ks - 1; }
 
 // ---------------------------------------------------------------- packing
-__global__ void absmax_kernel(const float *__restrict__ x, int64_t n, unsigned *__restrict__ out) {
+// max |x| into *out (as uint: m >= 0 orders like its bits).  One atomic per
+// BLOCK after an LDS reduction, and at most 512 blocks with >= 8 elements
+// per thread: per-wave atomics on the one address serialised in L2 (4096 of
+// them for a 1-M-float input: 33 us, profiles/r04b/prof_A_kernel_stats.md)
+__device__ __forceinline__ void absmax_commit(float m, unsigned *out) {
+    __shared__ float red[4];
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ x, int64_t n, unsigned *__restrict__ out) {
     float m = 0.0f;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
         m = fmaxf(m, fabsf(x[i]));
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // m >= 0: uint order
+    absmax_commit(m, out);
 }
 
-__global__ void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4, unsigned *__restrict__ out) {
+__global__ __launch_bounds__(256) void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4,
+                                                         unsigned *__restrict__ out) {
     float m = 0.0f;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         const float4 v = x[i];
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    absmax_commit(m, out);
 }
 
 // Activation records: value v(s, ch, y, x) -> [S][NCc*HALVES][4 pieces][Hp][Wp][16 B],
@@ -1101,11 +1112,11 @@ extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out,
     unsigned *o = reinterpret_cast<unsigned *>(out);
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0) {
         const int64_t n4 = n / 4;
-        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n4, 256), 4096);
+        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n4, 256 * 8), 512);
         hipLaunchKernelGGL(absmax_vec_kernel, dim3(blocks), dim3(256), 0, s,
                            reinterpret_cast<const float4 *>(x), n4, o);
     } else {
-        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n, 256), 4096);
+        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n, 256 * 8), 512);
         hipLaunchKernelGGL(absmax_kernel, dim3(blocks), dim3(256), 0, s, x, n, o);
     }
     TMR_CHECK_LAUNCH();

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -31,7 +32,8 @@ import torch
 
 from . import exp_table, host
 from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
-                   SPLIT_TILED_OUT, XCORR_ALGOS, TMRError, call, load, ptr, require_gpu, stream)
+                   SPLIT_TILED_OUT, UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr, require_gpu,
+                   stream)
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
@@ -301,23 +303,58 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     return out
 
 
-def _h2d(arr: np.ndarray, device, dtype=None) -> torch.Tensor:
+# graph capture of TMREngine.detect's forward (_DetectGraph): while set, every
+# host input staged by _h2d is kept under its tag, so that a replay can refill
+# the same pinned buffer the captured copy node reads
+_capture = threading.local()
+
+
+def _h2d(arr: np.ndarray, device, dtype=None, tag: Optional[str] = None) -> torch.Tensor:
     """A small host array on the device WITHOUT a stream sync: staged through
     torch's caching pinned-memory allocator and copied non_blocking (the
     allocator keeps the pinned block until the copy's stream event has
     completed).  A pageable `.to(device)` synchronises the stream, leaving the
-    GPU idle while the host prepares the next launches."""
+    GPU idle while the host prepares the next launches.  Inside a graph
+    capture the pinned buffer is kept under `tag` (the replay rewrites it)."""
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if dtype is not None:
         t = t.to(dtype)
     device = torch.device(device)
     if device.type != "cuda":
         return t.to(device)
-    return t.pin_memory().to(device, non_blocking=True)
+    slots = getattr(_capture, "slots", None)
+    if slots is None:
+        return t.pin_memory().to(device, non_blocking=True)
+    # capture: the pinned buffer was allocated before the capture began (no
+    # host allocation inside it) and is refilled before every replay
+    pinned = slots.get(tag) if tag is not None else None
+    if pinned is None or pinned.numel() * pinned.element_size() != t.numel() * t.element_size():
+        raise TMRError(f"host input {tag!r} inside a graph capture has no pre-allocated slot")
+    np.copyto(pinned.numpy(), t.numpy().reshape(-1).view(pinned.numpy().dtype))
+    _capture.used.add(tag)
+    return pinned.view(t.dtype).reshape(t.shape).to(device, non_blocking=True)
 
 
-def _units_to_device(units: np.ndarray, device) -> torch.Tensor:
-    return _h2d(units.view(np.uint8), device)
+def _units_to_device(units: np.ndarray, device, tag: Optional[str] = None) -> torch.Tensor:
+    return _h2d(units.view(np.uint8), device, tag=tag)
+
+
+class _DetectGraph:
+    """One captured detect forward (projection ... peaks) for a fixed launch
+    signature: the inputs are a static feature buffer and the pinned host
+    slots of its tagged host inputs; the outputs the peak finder's static
+    buffers.  A replay refills both and launches the whole forward at once."""
+
+    def __init__(self, graph, feats, slots, outputs, last):
+        self.graph, self.feats, self.slots, self.outputs, self.last = graph, feats, slots, outputs, last
+
+    def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray]):
+        for tag, arr in host.items():
+            dst = self.slots[tag].numpy()
+            np.copyto(dst, np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
+        self.feats.copy_(feats)
+        self.graph.replay()
+        return self.outputs
 
 
 class TMREngine:
@@ -359,6 +396,9 @@ class TMREngine:
         self.reuse_image_work = False
         self._fp_memo = None
         self._acc0_memo = None
+        self._graphs: Dict[tuple, _DetectGraph] = {}
+        self._graph_seen: Dict[tuple, int] = {}
+        self.last_graph = None
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -558,9 +598,9 @@ class TMREngine:
         cfg = self.cfg
         units, tfl, mh, mw = host.build_units(unit_boxes, unit_image, H, W, C, cfg.template_type)
         dev = fp.device
-        units_d = _units_to_device(units, dev)
+        units_d = _units_to_device(units, dev, tag="units")
         img_units = host.image_ranges(unit_image, B)  # units are sorted by image
-        img_units_d = _h2d(np.asarray(img_units), dev)
+        img_units_d = _h2d(np.asarray(img_units), dev, tag="img_units")
         tmpl = torch.empty(max(tfl, 1), device=dev, dtype=torch.float32)
         call("tmr_templates", ptr(fp), B, C, H, W, ptr(units_d), U, mh, mw, ptr(tmpl), stream())
         Co = 1 if cfg.squeeze else C
@@ -623,7 +663,7 @@ class TMREngine:
         U, C1, H, W = f_tm.shape
         dev = f_tm.device
         C0 = fp.shape[1] if cfg.fusion else 0
-        ui = _h2d(np.asarray(unit_image, np.int32), dev)
+        ui = _h2d(np.asarray(unit_image, np.int32), dev, tag="unit_image")
         src0 = fp if cfg.fusion else None
         if cfg.decoder_num_layer == 1:
             B = fp.shape[0]
@@ -789,7 +829,7 @@ class TMREngine:
                 self._fp_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), pkey, fp,
                                  tuple(weakref.ref(t) for t in params))
         if self.cfg.no_matcher:
-            ui = _h2d(np.asarray(unit_image, np.int64), fp.device)
+            ui = _h2d(np.asarray(unit_image, np.int64), fp.device, tag="unit_image64")
             f_tm = fp.index_select(0, ui).contiguous()
             relu = torch.relu(f_tm) if want_aux else None
         else:
@@ -818,7 +858,7 @@ class TMREngine:
         H, W = o.shape[-2:]
         dev = o.device
         cap = H * W
-        prm = _h2d(params.view(np.uint8), dev)
+        prm = _h2d(params.view(np.uint8), dev, tag="peak_params")
         prob = torch.empty((U, H, W), device=dev, dtype=torch.float32)
         logits = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         box = torch.empty((U * cap, 4), device=dev, dtype=torch.float32)
@@ -865,6 +905,61 @@ class TMREngine:
                 K.append(keep[s:e])
         return (L, Bx, R, K) if want_keep else (L, Bx, R)
 
+    # detect's forward (projection ... peaks) as a replayed HIP graph when
+    # the same launch signature recurs (the reference's per-image loop at one
+    # image size and recurring template sizes): the host then issues ONE
+    # launch instead of ~30, and the GPU no longer idles while Python prepares
+    # them (config A: 0.38 of 2.95 ms per image, profiles/r04b/).  A signature
+    # is captured the second time it is seen; up to GRAPH_MAX_UNITS units (the
+    # graph's memory pool holds every intermediate) and GRAPH_CACHE entries.
+    use_graphs = True
+    GRAPH_MAX_UNITS = 32
+    GRAPH_CACHE = 8
+
+    def _graph_signature(self, feats: torch.Tensor, units: np.ndarray, unit_image, ablation_b, ablation_c):
+        if not (self.use_graphs and feats.is_cuda and len(unit_image) <= self.GRAPH_MAX_UNITS):
+            return None
+        if self.decoder_events is not None or self.xcorr_events is not None or self.reuse_image_work:
+            return None  # timed runs record events around single launches; the module API reuses memos
+        return (tuple(feats.shape), feats.dtype, str(feats.device), tuple(int(i) for i in unit_image),
+                tuple(units["ht"].tolist()), tuple(units["wt"].tolist()), tuple(sorted(vars(self.cfg).items())),
+                self.fold_proj,
+                self.share_fp_half, self.xcorr_algo, self.out_bf16, TMREngine.exp_mode,
+                bool(ablation_b), bool(ablation_c),
+                tuple((k, t.data_ptr(), t._version) for k, t in sorted(self.P.items())))
+
+    @staticmethod
+    def _detect_host_inputs(units, unit_image, B, params) -> Dict[str, np.ndarray]:
+        """The tagged host inputs of detect's forward, as _h2d stages them."""
+        return {"units": units.view(np.uint8), "img_units": np.asarray(host.image_ranges(unit_image, B)),
+                "unit_image": np.asarray(unit_image, np.int32), "unit_image64": np.asarray(unit_image, np.int64),
+                "peak_params": params.view(np.uint8)}
+
+    def _forward_peaks(self, feats, unit_image, boxes, params):
+        r = self.forward_units(feats, unit_image, boxes)
+        logits, box, ref, counts, _ = self.peaks(r["o"], r["b"], params)
+        return logits, box, ref, counts
+
+    def _capture_detect(self, feats, unit_image, boxes, params, host_in):
+        """Capture _forward_peaks on a static copy of feats (caches built by
+        the eager call that preceded).  None if capture fails (eager then)."""
+        static = feats.detach().float().contiguous().clone()
+        slots = {t: torch.empty(a.nbytes, dtype=torch.uint8).pin_memory() for t, a in host_in.items()}
+        torch.cuda.synchronize(feats.device)
+        graph = torch.cuda.CUDAGraph()
+        _capture.slots, _capture.used = slots, set()
+        try:
+            with torch.cuda.graph(graph):
+                out = self._forward_peaks(static, unit_image, boxes, params)
+            used = _capture.used
+        except Exception:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
+            return None
+        finally:
+            _capture.slots = _capture.used = None
+        slots = {t: v for t, v in slots.items() if t in used}
+        last = {k: v for k, v in vars(self).items() if k.startswith("last_")}
+        return _DetectGraph(graph, static, slots, out, last)
+
     def detect(self, feats: torch.Tensor, exemplars, cls_ths: float, iou_threshold: float,
                ablation_b: bool = False, ablation_c: bool = False):
         """The reference's multi-exemplar inference (demo.py:106-130,
@@ -879,13 +974,35 @@ class TMREngine:
         B, E = ex.shape[:2]
         unit_image = np.repeat(np.arange(B), E)
         boxes = ex.reshape(B * E, 4)
-        r = self.forward_units(feats, unit_image, boxes)
-        o, b = r["o"], r["b"]
-        H, W = o.shape[-2:]
+        require_gpu(feats, "features")
+        Hin, Win = feats.shape[-2:]
+        H, W = (2 * Hin, 2 * Win) if self.cfg.feature_upsample else (Hin, Win)
         params = host.peak_params(boxes, H, W, cls_ths, self.cfg.box_reg, ablation_b, ablation_c)
-        logits, box, ref, counts, _ = self.peaks(o, b, params)
+        C = int(self.P["input_proj.0.weight"].shape[0])
+        units = host.build_units(boxes, unit_image, H, W, C, self.cfg.template_type)[0] \
+            if not self.cfg.no_matcher else np.zeros(0, UNIT_DTYPE)
+        sig = self._graph_signature(feats, units, unit_image, ablation_b, ablation_c)
+        g = self._graphs.get(sig) if sig is not None else None
+        self.last_graph = "replay" if g is not None else "eager"
+        if g is None and sig is not None:
+            self._graph_seen[sig] = self._graph_seen.get(sig, 0) + 1
+            if self._graph_seen[sig] >= 2:
+                g = self._capture_detect(feats, unit_image, boxes, params, self._detect_host_inputs(
+                    units, unit_image, B, params))
+                if g is not None:
+                    if len(self._graphs) >= self.GRAPH_CACHE:
+                        self._graphs.pop(next(iter(self._graphs)))
+                    self._graphs[sig] = g
+                    self.last_graph = "captured"
+        if g is not None:
+            host_in = self._detect_host_inputs(units, unit_image, B, params)
+            logits, box, ref, counts = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
+            for k, v in g.last.items():
+                setattr(self, k, v)
+        else:
+            logits, box, ref, counts = self._forward_peaks(feats, unit_image, boxes, params)
         counts_host = counts.cpu().numpy()  # torch.where-style sync (TM_utils.py:254)
         U = B * E
-        unit_off = torch.arange(U, device=o.device, dtype=torch.int64) * (H * W)
+        unit_off = torch.arange(U, device=feats.device, dtype=torch.int64) * (H * W)
         seg = np.arange(0, U + 1, E, dtype=np.int64)
         return self.nms(logits, box, ref, counts, counts_host, unit_off, seg, iou_threshold)

@@ -899,3 +899,48 @@ def test_nms_worst_case_dense_candidates():
         assert np.array_equal(K[img].cpu().numpy(), keep), img
         assert bits_equal(Bx[img].cpu().numpy(), cb[keep])
         assert bits_equal(L[img].cpu().numpy()[:, 0], cs[keep])
+
+
+def test_detect_graph_replay_matches_eager():
+    """TMREngine.detect's HIP-graph path: the second call of a launch
+    signature captures the forward (projection ... peaks), later calls replay
+    it with refilled host inputs.  Every call -- eager, capture, replay with
+    other features, with other exemplar boxes of the same template sizes, and
+    after a weight update (a new signature) -- returns exactly the eager
+    engine's detections."""
+    cin, emb, hf, B, E = 32, 64, 16, 2, 3
+    P = synth.reference_state_dict(12, cin=cin, emb=emb, obj_bias=0.4)
+    Pd = {k: cuda(v) for k, v in P.items()}
+    eng = tmr_amd.TMREngine(Pd, tmr_amd.PathConfig(emb_dim=emb))
+    ref = tmr_amd.TMREngine({k: v.clone() for k, v in Pd.items()}, tmr_amd.PathConfig(emb_dim=emb))
+    ref.use_graphs = False
+    ex0, _ = synth.exemplar_set(40, B, E, 2 * hf, 2 * hf, 3, 7)
+
+    def shifted(ex, d):  # same template sizes, other boxes (moved only where they stay inside)
+        out = ex.copy()
+        ok = (out[..., 0] + d >= 0.0) & (out[..., 2] + d <= 1.0)
+        out[..., 0] = np.where(ok, out[..., 0] + d, out[..., 0])
+        out[..., 2] = np.where(ok, out[..., 2] + d, out[..., 2])
+        return out.astype(np.float32)
+
+    cases = [(41, ex0), (41, ex0), (42, ex0), (43, shifted(ex0, 0.01)), (44, shifted(ex0, -0.02))]
+    modes = []
+    for seed, ex in cases:
+        feats = cuda(synth.sam_features(seed, B, cin, hf, hf))
+        got = eng.detect(feats, ex, 0.5, 0.5)
+        modes.append(eng.last_graph)
+        want = ref.detect(feats, ex, 0.5, 0.5)
+        for g_, w_ in zip(got, want):
+            for a, b in zip(g_, w_):
+                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (seed, eng.last_graph)
+    assert modes[0] == "eager" and modes[1] == "captured" and modes[2:] == ["replay"] * 3, modes
+    # a weight update is a new signature: eager again, never a stale replay
+    with torch.no_grad():
+        eng.P["objectness_head.head.0.bias"].add_(0.1)
+        ref.P["objectness_head.head.0.bias"].add_(0.1)
+    feats = cuda(synth.sam_features(45, B, cin, hf, hf))
+    got, want = eng.detect(feats, ex0, 0.5, 0.5), ref.detect(feats, ex0, 0.5, 0.5)
+    assert eng.last_graph == "eager"
+    for g_, w_ in zip(got, want):
+        for a, b in zip(g_, w_):
+            assert bits_equal(a.cpu().numpy(), b.cpu().numpy())
