@@ -14,7 +14,8 @@
  *  - Every call is asynchronous on `stream` (a hipStream_t, passed as void*;
  *    NULL = the null stream) and returns 0 or a negative TMR_E* code; nothing
  *    throws across the ABI.  tmr_strerror() names the code.
- *  - No global mutable state: calls are reentrant across streams/devices.
+ *  - No global mutable state (beyond an idempotent per-(device, kernel) cache of
+ *    the LDS-size attribute): calls are reentrant across streams/devices.
  *  - "units" are (image, exemplar) matching units, described by a device
  *    array of tmr_unit_t built on the host (the reference sizes templates on
  *    the host too: template_matching.py:56-73 runs Python math on 0-d

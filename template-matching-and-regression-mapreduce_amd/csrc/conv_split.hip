@@ -729,7 +729,7 @@ int launch_split(SArgs a, hipStream_t s) {
     static_assert(lds <= 160 * 1024, "LDS");
     static_assert((4 * 8 * NHEAD * 16 + BM * (NHEAD + 1)) * 4 <= lds, "epilogue scratch");
     auto kern = split_conv_kernel<KS, PREC, EPI>;
-    if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+    if (tmr_set_max_lds((const void *)kern, lds) !=
         hipSuccess)
         return TMR_E_HIP;
     const int64_t blocks = (int64_t)a.NT * a.MT * a.U;

@@ -337,7 +337,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     const size_t lds = sizeof(uint64_t) * (size_t)max_nb;
     auto rk = reduce_strip_kernel;
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        tmr_set_max_lds((const void *)rk, lds) !=
             hipSuccess)
         return TMR_E_HIP;
     hipLaunchKernelGGL(sort_boxes_kernel, dim3((unsigned)std::min<int64_t>(tmr_cdiv(max_cand, 256), 1024), G),

@@ -1,6 +1,10 @@
 // Shared helpers for the libtmr.so HIP sources (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -21,10 +25,22 @@ static inline hipStream_t tmr_stream(void *s) { return reinterpret_cast<hipStrea
 
 static inline int64_t tmr_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// host-side A/B switch of a measured variant (documented where it is read)
-static inline int tmr_env_int(const char *name, int dflt) {
-    const char *v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel):
+// the attribute is idempotent and the call is no stream operation, so a
+// launch replayed inside a HIP graph capture must not re-issue it (the
+// runtime refuses non-stream calls during a global-mode capture).  The only
+// process-wide state of the library: a cache of an idempotent setting.
+static inline hipError_t tmr_set_max_lds(const void *fn, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = done.find({dev, fn});
+    if (it != done.end() && it->second >= bytes) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done[{dev, fn}] = bytes;
+    return e;
 }
 
 // Near-correctly-rounded fp32 exp / sigmoid: double evaluation, one rounding.

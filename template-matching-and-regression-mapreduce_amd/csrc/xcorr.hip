@@ -703,16 +703,24 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
             }
 #pragma unroll
             for (int nk = 0; nk < NK; ++nk) {
+                // term-major over the wave's tiles: each tile's three
+                // products (th.fh, th.fl, tl.fh, in that order per tile as
+                // before) are NTW MFMAs apart, not back to back on one
+                // accumulator (a dependent MFMA waits for its predecessor)
+                V bh[NTW], bl[NTW];
 #pragma unroll
                 for (int t = 0; t < NTW; ++t) {
                     const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-                    const V bh = *reinterpret_cast<const V *>(rh + colb);
-                    acc[t] = xmma(ch[nk], bh, acc[t]);
-                    if (SPLIT) {
-                        const V bl = *reinterpret_cast<const V *>(rl + colb);
-                        acc[t] = xmma(ch[nk], bl, acc[t]);
-                        acc[t] = xmma(cl[nk], bh, acc[t]);
-                    }
+                    bh[t] = *reinterpret_cast<const V *>(rh + colb);
+                    if (SPLIT) bl[t] = *reinterpret_cast<const V *>(rl + colb);
+                }
+#pragma unroll
+                for (int t = 0; t < NTW; ++t) acc[t] = xmma(ch[nk], bh[t], acc[t]);
+                if (SPLIT) {
+#pragma unroll
+                    for (int t = 0; t < NTW; ++t) acc[t] = xmma(ch[nk], bl[t], acc[t]);
+#pragma unroll
+                    for (int t = 0; t < NTW; ++t) acc[t] = xmma(cl[nk], bh[t], acc[t]);
                 }
             }
         }
@@ -916,7 +924,7 @@ static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
                          const _Float16 *trows, const int32_t *texp) {
     const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>;
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        tmr_set_max_lds(kfn, lds) != hipSuccess)
         return TMR_E_HIP;
     hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
                        texp, a.out, a.units);
@@ -1049,7 +1057,7 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
         const void *kfn = !rows ? (const void *)xcorr_kernel
                           : narrow ? (const void *)xcorr_rows_kernel<15> : (const void *)xcorr_rows_kernel<31>;
         if (lds > 64 * 1024 &&
-            hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            tmr_set_max_lds(kfn, lds) != hipSuccess)
             return TMR_E_HIP;
         dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
         if (rows && narrow)

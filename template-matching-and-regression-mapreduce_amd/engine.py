@@ -399,6 +399,7 @@ class TMREngine:
         self._graphs: Dict[tuple, _DetectGraph] = {}
         self._graph_seen: Dict[tuple, int] = {}
         self.last_graph = None
+        self.last_graph_error = None
         self.last_decoder_flops = 0.0
         self.last_shared_flops = 0.0
         self.last_decoder_algo = None
@@ -952,7 +953,8 @@ class TMREngine:
             with torch.cuda.graph(graph):
                 out = self._forward_peaks(static, unit_image, boxes, params)
             used = _capture.used
-        except Exception:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
+        except Exception as err:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
+            self.last_graph_error = f"{type(err).__name__}: {err}"
             return None
         finally:
             _capture.slots = _capture.used = None

@@ -933,7 +933,8 @@ def test_detect_graph_replay_matches_eager():
         for g_, w_ in zip(got, want):
             for a, b in zip(g_, w_):
                 assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (seed, eng.last_graph)
-    assert modes[0] == "eager" and modes[1] == "captured" and modes[2:] == ["replay"] * 3, modes
+    assert modes[0] == "eager" and modes[1] == "captured" and modes[2:] == ["replay"] * 3, \
+        (modes, eng.last_graph_error)
     # a weight update is a new signature: eager again, never a stale replay
     with torch.no_grad():
         eng.P["objectness_head.head.0.bias"].add_(0.1)
