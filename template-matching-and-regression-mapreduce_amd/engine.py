@@ -959,7 +959,7 @@ class TMREngine:
         finally:
             _capture.slots = _capture.used = None
         slots = {t: v for t, v in slots.items() if t in used}
-        last = {k: v for k, v in vars(self).items() if k.startswith("last_")}
+        last = {k: v for k, v in vars(self).items() if k.startswith("last_") and not k.startswith("last_graph")}
         return _DetectGraph(graph, static, slots, out, last)
 
     def detect(self, feats: torch.Tensor, exemplars, cls_ths: float, iou_threshold: float,
