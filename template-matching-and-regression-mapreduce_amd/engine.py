@@ -803,11 +803,110 @@ class TMREngine:
     def _acc0_store(self, feats, split, H, W, acc0):
         self._acc0_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), split, (H, W), acc0)
 
+    def _memo_hit(self, feats: torch.Tensor):
+        """(fp, acc0) kept for this feature tensor by an earlier call, or None."""
+        m, a = self._fp_memo, self._acc0_memo
+        params = (self.P["input_proj.0.weight"], self.P["input_proj.0.bias"])
+        pkey = (_version_key(params), self.cfg.precision, self.cfg.feature_upsample)
+        if self._same_image(m, feats) and m[3] == pkey and all(r() is t for r, t in zip(m[5], params)) and \
+                self._same_image(a, feats):
+            return m[4], a[3:6]
+        return None
+
+    def _rebind_memos(self, feats: torch.Tensor, fp: torch.Tensor, acc0_memo: tuple):
+        """Point the per-image memos at (fp, acc0) for `feats`; acc0_memo =
+        (split, (H, W), acc0) as _acc0_store keeps them."""
+        params = (self.P["input_proj.0.weight"], self.P["input_proj.0.bias"])
+        pkey = (_version_key(params), self.cfg.precision, self.cfg.feature_upsample)
+        self._fp_memo = (weakref.ref(feats), feats._version, feats.data_ptr(), pkey, fp,
+                         tuple(weakref.ref(t) for t in params))
+        self._acc0_memo = (weakref.ref(feats), feats._version, feats.data_ptr()) + tuple(acc0_memo)
+
+    def _forward_units_graphed(self, feats, unit_image, unit_boxes, want_aux):
+        """The module API's per-exemplar forward (reuse_image_work) as a
+        replayed HIP graph once its signature recurs.  Two graphs per shape:
+        the image's first call (projection + fp half + correlation + heads;
+        its fp / acc0 become the image's memo) and the later calls on the same
+        features (correlation + heads off that memo).  Outputs are cloned: a
+        caller may keep one exemplar's maps while the next replay runs."""
+        if not (self.use_graphs and feats.is_cuda and len(unit_image) <= self.GRAPH_MAX_UNITS) or \
+                self.decoder_events is not None or self.xcorr_events is not None or self.cfg.no_matcher or \
+                self.cfg.decoder_num_layer != 1 or not (self.cfg.fusion and self.fold_proj):
+            return None
+        B, Cin, Hin, Win = feats.shape
+        H, W = (2 * Hin, 2 * Win) if self.cfg.feature_upsample else (Hin, Win)
+        C = int(self.P["input_proj.0.weight"].shape[0])
+        boxes = np.asarray(unit_boxes, np.float32).reshape(-1, 4)
+        units = host.build_units(boxes, unit_image, H, W, C, self.cfg.template_type)[0]
+        hit = self._memo_hit(feats)
+        base = self._graph_signature(feats, units, unit_image, False, False, module=True)
+        if base is None:
+            return None
+        sig = base + (bool(want_aux), None if hit is None else (hit[0].data_ptr(), hit[1][2].data_ptr()))
+        g = self._graphs.get(sig)
+        self.last_graph = "replay" if g is not None else "eager"
+        if g is None:
+            self._graph_seen[sig] = self._graph_seen.get(sig, 0) + 1
+            if self._graph_seen[sig] < 2:
+                return None
+            g = self._capture_module(feats, unit_image, boxes, want_aux, hit, self._detect_host_inputs(
+                units, unit_image, B, np.zeros(0, np.uint8)))
+            if g is None:
+                return None
+            if len(self._graphs) >= self.GRAPH_CACHE:
+                self._graphs.pop(next(iter(self._graphs)))
+            self._graphs[sig] = g
+            self.last_graph = "captured"
+        host_in = self._detect_host_inputs(units, unit_image, B, np.zeros(0, np.uint8))
+        out = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
+        for k, v in g.last.items():
+            setattr(self, k, v)
+        if hit is None:  # this image's memo: the first-call graph's fp / acc0
+            self._rebind_memos(feats, g.fp, g.acc0)
+        return {k: (v.clone() if isinstance(v, torch.Tensor) and k != "fp" else v) for k, v in out.items()}
+
+    def _capture_module(self, feats, unit_image, boxes, want_aux, hit, host_in):
+        static = feats.detach().float().contiguous().clone()
+        slots = {t: torch.empty(a.nbytes, dtype=torch.uint8).pin_memory() for t, a in host_in.items() if a.nbytes}
+        saved = (self._fp_memo, self._acc0_memo)
+        if hit is not None:
+            self._rebind_memos(static, hit[0], hit[1])  # the capture reads the memo buffers
+        else:
+            self._fp_memo = self._acc0_memo = None
+        torch.cuda.synchronize(feats.device)
+        graph = torch.cuda.CUDAGraph()
+        _capture.slots, _capture.used = slots, set()
+        try:
+            with torch.cuda.graph(graph):
+                out = self._forward_units_eager(static, unit_image, boxes, want_aux)
+            used = _capture.used
+            fp_acc0 = (self._fp_memo[4], self._acc0_memo[3:6]) if hit is None else (None, None)
+        except Exception as err:  # noqa: BLE001 -- stay eager
+            self.last_graph_error = f"{type(err).__name__}: {err}"
+            self._fp_memo, self._acc0_memo = saved
+            return None
+        finally:
+            _capture.slots = _capture.used = None
+        self._fp_memo, self._acc0_memo = saved
+        g = _DetectGraph(graph, static, {t: v for t, v in slots.items() if t in used}, out,
+                         {k: v for k, v in vars(self).items() if k.startswith("last_") and
+                          not k.startswith("last_graph")})
+        g.fp, g.acc0 = fp_acc0
+        return g
+
     def forward_units(self, feats: torch.Tensor, unit_image: Sequence[int], unit_boxes,
                       want_aux: bool = False):
         """One matching_net forward per unit (image unit_image[u], exemplar
         unit_boxes[u]).  Returns dict(o, b, f_tm_relu, f0, fp)."""
         unit_image = [int(i) for i in unit_image]
+        if self.reuse_image_work and getattr(_capture, "slots", None) is None:
+            r = self._forward_units_graphed(feats, unit_image, unit_boxes, want_aux)
+            if r is not None:
+                return r
+        return self._forward_units_eager(feats, unit_image, unit_boxes, want_aux)
+
+    def _forward_units_eager(self, feats: torch.Tensor, unit_image: Sequence[int], unit_boxes,
+                             want_aux: bool = False):
         m = self._fp_memo
         # the projection memo follows the input_proj parameters' storage,
         # version AND identity (as _PackCache), and the path options that
@@ -917,11 +1016,13 @@ class TMREngine:
     GRAPH_MAX_UNITS = 32
     GRAPH_CACHE = 8
 
-    def _graph_signature(self, feats: torch.Tensor, units: np.ndarray, unit_image, ablation_b, ablation_c):
+    def _graph_signature(self, feats: torch.Tensor, units: np.ndarray, unit_image, ablation_b, ablation_c,
+                         module: bool = False):
         if not (self.use_graphs and feats.is_cuda and len(unit_image) <= self.GRAPH_MAX_UNITS):
             return None
-        if self.decoder_events is not None or self.xcorr_events is not None or self.reuse_image_work:
-            return None  # timed runs record events around single launches; the module API reuses memos
+        if self.decoder_events is not None or self.xcorr_events is not None or \
+                (self.reuse_image_work and not module):
+            return None  # timed runs record events around single launches; detect has no image memo
         return (tuple(feats.shape), feats.dtype, str(feats.device), tuple(int(i) for i in unit_image),
                 tuple(units["ht"].tolist()), tuple(units["wt"].tolist()), tuple(sorted(vars(self.cfg).items())),
                 self.fold_proj,

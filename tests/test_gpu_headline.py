@@ -376,3 +376,38 @@ def test_module_reuse_follows_inputs_and_weights():
         fd.mul_(1.1)
     check(feats * np.float32(1.1), "features updated in place")
     check(synth.sam_features(99, 1, feats.shape[1], feats.shape[2], feats.shape[3]), "new tensor")
+
+
+def test_module_graph_replay_matches_eager():
+    """The module API's per-exemplar forwards (demo.py:106-130 call form) as
+    replayed HIP graphs: the first call on an image and the later calls on
+    the same features each get their graph once their signature recurs.  Over
+    several images (same shapes and template sizes, new feature values, new
+    exemplar positions) every output -- objectness, regression, relu(f_TM),
+    f[0] -- is bit-identical to the eager engine's, outputs kept from an
+    earlier exemplar are not overwritten by later replays, and graphs are
+    actually replayed."""
+    args, model, P, feats0, ex0 = _model_and_inputs(seed=31, E=3, hf=16, cin=32, emb=48)
+    args2, ref_model, _, _, _ = _model_and_inputs(seed=31, E=3, hf=16, cin=32, emb=48)
+    ref_model.engine().use_graphs = False
+    modes = []
+    for img in range(4):
+        feats = cuda(synth.sam_features(60 + img, 1, 32, 16, 16))
+        ex = ex0.copy()
+        ex[..., [0, 2]] += 0.003 * img  # same template sizes, other positions
+        exemplars = [[e.unsqueeze(0)] for e in cuda(ex[0])]
+        kept = []
+        with torch.no_grad():
+            for exemplar in exemplars:
+                out = model(feats, exemplar)
+                modes.append(model.engine().last_graph)
+                kept.append(out)
+                want = ref_model(feats, exemplar)
+                for g_, w_ in zip(out[:3], want[:3]):
+                    assert bits_equal(g_[0].cpu().numpy(), w_[0].cpu().numpy()), (img, modes[-1])
+                assert bits_equal(out[3].cpu().numpy(), want[3].cpu().numpy())
+        # the first exemplar's maps, kept while the later ones replayed, are intact
+        again = ref_model(feats, exemplars[0])
+        assert bits_equal(kept[0][0][0].cpu().numpy(), again[0][0].cpu().numpy())
+        assert bits_equal(kept[0][2][0].cpu().numpy(), again[2][0].cpu().numpy())
+    assert "replay" in modes and "captured" in modes, (modes, model.engine().last_graph_error)
