@@ -361,12 +361,14 @@ def main():
                 driver.all_gather_detections(counts, rows)
             return L
 
-    # detect path at small batches: the forward is replayed as a HIP graph
-    # once its signature recurs (TMREngine.use_graphs); a replay records no
+    # detect path at small batches and the module path: the forward is
+    # replayed as a HIP graph once its signature recurs (TMREngine.use_graphs); a replay records no
     # per-kernel events, so the kernels' HIP-event times then come from one
     # eager step after the timed loop (same kernels, same stream)
     eng.use_graphs = not a.no_graphs
-    graphs = a.path == "detect" and eng.use_graphs and B * E <= eng.GRAPH_MAX_UNITS
+    if a.path == "module":  # the module's engine replays each exemplar's forward
+        model.engine().use_graphs = not a.no_graphs
+    graphs = eng.use_graphs and (a.path == "module" or B * E <= eng.GRAPH_MAX_UNITS)
     for _ in range(a.warmup):
         step()
     if a.path == "module":

@@ -17,6 +17,7 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
            (no MALL / HBM traffic)
 
     python profiles/heads_variants.py build [variants...]   # here, on the CPU
+    python profiles/heads_variants.py build-rev NAME REV FILE  # FILE of csrc/ as of git REV
     python profiles/heads_variants.py clean
 """
 import os
@@ -80,7 +81,7 @@ def variant_source(name: str, src: str) -> str:
 VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma", "l2dma"]
 
 
-def build(names):
+def build(names, rev_file=None):
     for name in names:
         scratch = os.path.join(PKG, f"build_var_{name}")
         src_dir = os.path.join(scratch, "csrc")
@@ -91,7 +92,12 @@ def build(names):
             if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile":
                 p = os.path.join(src_dir, f)
                 txt = open(p).read().replace("../../include/", "../../../include/")
-                if f == "conv_split.hip":
+                if rev_file is not None and f == rev_file[1]:
+                    rel = os.path.relpath(os.path.join(CSRC, f), REPO)
+                    txt = subprocess.run(["git", "-C", REPO, "show", f"{rev_file[0]}:{rel}"], check=True,
+                                         capture_output=True, text=True).stdout
+                    txt = txt.replace("../../include/", "../../../include/")
+                elif rev_file is None and f == "conv_split.hip":
                     txt = variant_source(name, txt)
                 with open(p, "w") as fh:
                     fh.write(txt)
@@ -102,14 +108,15 @@ def build(names):
 
 
 def clean():
-    for name in VARIANTS:
-        p = os.path.join(PKG, f"libtmr_{name}.so")
-        if os.path.exists(p):
-            os.remove(p)
+    for f in os.listdir(PKG):
+        if f.startswith("libtmr_") and f.endswith(".so"):
+            os.remove(os.path.join(PKG, f))
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "clean":
         clean()
+    elif len(sys.argv) > 1 and sys.argv[1] == "build-rev":
+        build([sys.argv[2]], (sys.argv[3], sys.argv[4]))
     else:
         build(sys.argv[2:] or VARIANTS)
