@@ -72,3 +72,32 @@ def test_launcher_starts_children_and_returns_their_status(tmp_path):
     assert r.returncode == 3, r.stderr
     got = rec.read_text()
     assert "--nproc-per-node=2" in got and got.endswith("--gpus 2 --steps 1")
+
+
+def test_pmc_fields_tied_to_kernel_sources(tmp_path, monkeypatch):
+    """a committed PMC record's counters are printed only while
+    the kernel's sources are the ones it was collected on (buildinfo digest);
+    otherwise load_pmc returns None with the reason."""
+    import json
+    b = _bench()
+    from tmr_amd import buildinfo
+    rec = {"hbm_bytes_per_launch": 1.0, "source_digest": buildinfo.source_digest("heads")}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"round": "t", "configs": {"B": {"heads": rec}}}))
+    monkeypatch.setattr(b, "PMC_FILE", str(p))
+    got, why = b.load_pmc("B", "heads")
+    assert why is None and got["hbm_bytes_per_launch"] == 1.0 and "round t" in got["source"]
+    rec["source_digest"] = "0" * 16
+    p.write_text(json.dumps({"round": "t", "configs": {"B": {"heads": rec}}}))
+    got, why = b.load_pmc("B", "heads")
+    assert got is None and "other kernel sources" in why
+    assert b.load_pmc("C", "heads") == (None, "no PMC record for this config")
+
+
+def test_frac_guard_nulls_fractions_above_one():
+    b = _bench()
+    out = {"roofline": {"frac": 0.2, "executed_frac": 1.3, "nested": {"x_frac": 2.0, "n": 5}}, "frac": 0.9}
+    hits = b.guard_fracs(out)
+    assert out["roofline"]["executed_frac"] is None and out["roofline"]["nested"]["x_frac"] is None
+    assert out["roofline"]["frac"] == 0.2 and out["frac"] == 0.9 and out["roofline"]["nested"]["n"] == 5
+    assert sorted(hits) == ["roofline.executed_frac=1.3", "roofline.nested.x_frac=2.0"]
