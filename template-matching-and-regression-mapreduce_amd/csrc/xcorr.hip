@@ -703,24 +703,16 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
             }
 #pragma unroll
             for (int nk = 0; nk < NK; ++nk) {
-                // term-major over the wave's tiles: each tile's three
-                // products (th.fh, th.fl, tl.fh, in that order per tile as
-                // before) are NTW MFMAs apart, not back to back on one
-                // accumulator (a dependent MFMA waits for its predecessor)
-                V bh[NTW], bl[NTW];
 #pragma unroll
                 for (int t = 0; t < NTW; ++t) {
                     const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-                    bh[t] = *reinterpret_cast<const V *>(rh + colb);
-                    if (SPLIT) bl[t] = *reinterpret_cast<const V *>(rl + colb);
-                }
-#pragma unroll
-                for (int t = 0; t < NTW; ++t) acc[t] = xmma(ch[nk], bh[t], acc[t]);
-                if (SPLIT) {
-#pragma unroll
-                    for (int t = 0; t < NTW; ++t) acc[t] = xmma(ch[nk], bl[t], acc[t]);
-#pragma unroll
-                    for (int t = 0; t < NTW; ++t) acc[t] = xmma(cl[nk], bh[t], acc[t]);
+                    const V bh = *reinterpret_cast<const V *>(rh + colb);
+                    acc[t] = xmma(ch[nk], bh, acc[t]);
+                    if (SPLIT) {
+                        const V bl = *reinterpret_cast<const V *>(rl + colb);
+                        acc[t] = xmma(ch[nk], bl, acc[t]);
+                        acc[t] = xmma(cl[nk], bh, acc[t]);
+                    }
                 }
             }
         }
