@@ -1,9 +1,11 @@
 # PMC passes (one counter group per run, rocprofv3 --pmc, CSV) over one step of bench.py
 # for every config (A-E), one launch per kernel role (--no-xcorr-classes); assembled by
 # profiles/pmc_assemble.py into profiles/pmc_by_config.json (bench.py's roofline.traffic).
-# Run from the repo root: gpurun -- bash profiles/gpu_pmc.sh <label>
+# Run from the repo root: gpurun -- bash profiles/gpu_pmc.sh <label> [configs...]  (default B C D E A)
 set -o pipefail
 L=${1:-pmc}
+shift
+CFGS=${@:-B C D E A}
 mkdir -p gpurun_out/pmc_$L
 export TMPDIR=/tmp
 run() {  # run <name> <bench args> -- <counters...>
@@ -13,7 +15,7 @@ run() {  # run <name> <bench args> -- <counters...>
         python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-xcorr-classes "${args[@]}" > gpurun_out/pmc_$L/$name.log 2>&1
 }
 CORE="GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_LDS"
-for c in B C D E A; do
+for c in $CFGS; do
     run ${c}_fetch --config $c -- FETCH_SIZE || exit 1
     run ${c}_write --config $c -- WRITE_SIZE || exit 1
     run ${c}_core --config $c -- $CORE || exit 1
