@@ -262,3 +262,17 @@ def test_reference_exp_table_from_committed_blob(tmp_path):
 
 
 HEADER_FLIP = 128 + 4 * 40000  # a byte inside the offsets block
+
+
+def test_reference_exp_table_ensure_rebuilds_damaged(tmp_path):
+    """build()'s table step (exp_table.ensure): a present golden table is
+    kept, a damaged or missing one is re-expanded from the committed blob."""
+    from tmr_amd import exp_table
+    p = tmp_path / "exp_ref.bin"
+    assert exp_table.ensure(str(p)) == "expanded"
+    assert exp_table.ensure(str(p)) == "verified"
+    b = bytearray(p.read_bytes())
+    b[HEADER_FLIP] ^= 4
+    p.write_bytes(bytes(b))
+    assert exp_table.ensure(str(p)) == "expanded"
+    assert exp_table.payload_sha256(np.fromfile(p, np.uint8)) == exp_table.GOLDEN_PAYLOAD_SHA256
