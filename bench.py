@@ -342,8 +342,9 @@ def main():
                 for b in range(B):
                     image = feats_d[b:b + 1]
                     # the image's exemplar boxes arrive with it, as from the
-                    # reference's loader (fresh device tensors every image)
-                    ex_d = torch.from_numpy(ex[b]).to(dev)
+                    # reference's loader (fresh device tensors every image,
+                    # DataLoader(pin_memory=True) + non_blocking copy)
+                    ex_d = torch.from_numpy(ex[b]).pin_memory().to(dev, non_blocking=True)
                     pl, pb, pr = [], [], []
                     for exemplar in [[ex_d[e].unsqueeze(0)] for e in range(E)]:  # demo.py:106
                         po, preg, _, _ = model(image, exemplar)

@@ -23,26 +23,35 @@ from ._lib import UNIT_DTYPE, TMRError, call, ptr, require_gpu, stream
 from .engine import PathConfig, TMREngine, _h2d, _units_to_device
 
 
-# Host copies of exemplar tensors, keyed on the tensor object (weak
-# reference), its storage and its version: the callers pass the SAME exemplar
-# tensor to matching_net.forward and then to Get_pred_boxes (demo.py:111-112,
-# trainer.py:96-97), and the second device->host read would wait for the whole
-# forward to drain before the host can queue the decode.
+# Host copies of exemplar tensors.  The callers pass the SAME exemplar to
+# matching_net.forward and then to Get_pred_boxes (demo.py:111-112,
+# trainer.py:96-97), but as a fresh view each time (`exemplars[b][0]` builds a
+# new tensor object); a second device->host read would wait for the whole
+# forward to drain before the host can queue the decode.  So the memo is keyed
+# on the view's BASE tensor (weak reference: a new loader tensor at a reused
+# address is another object) and its version (shared by all views): the whole
+# small base is read once and every view of it is sliced on the host.
 _BOX_MEMO: "dict[int, tuple]" = {}
+_BASE_MAX = 4096  # elements of a base read whole (exemplar boxes: a few dozen)
 
 
 def _box_host(exemplar_coord) -> np.ndarray:
     if isinstance(exemplar_coord, torch.Tensor):
         t = exemplar_coord
-        key = id(t)
+        base = t._base if t._base is not None else t
+        if base.numel() > _BASE_MAX or base.device != t.device:
+            return t.detach().float().cpu().numpy().reshape(4)
+        key = id(base)
         hit = _BOX_MEMO.get(key)
-        if hit is not None and hit[0]() is t and hit[1] == (t._version, t.data_ptr()):
-            return hit[2].copy()
-        v = t.detach().float().cpu().numpy().reshape(4)
-        if len(_BOX_MEMO) > 4096:
-            _BOX_MEMO.clear()
-        _BOX_MEMO[key] = (weakref.ref(t), (t._version, t.data_ptr()), v.copy())
-        return v
+        if hit is None or hit[0]() is not base or hit[1] != (base._version, base.data_ptr()):
+            hb = base.detach().cpu()
+            if len(_BOX_MEMO) > 4096:
+                _BOX_MEMO.clear()
+            hit = (weakref.ref(base), (base._version, base.data_ptr()), hb)
+            _BOX_MEMO[key] = hit
+        hb = hit[2]
+        v = hb.as_strided(t.shape, t.stride(), hb.storage_offset() + t.storage_offset() - base.storage_offset())
+        return v.float().numpy().reshape(4).copy()
     return np.asarray(exemplar_coord, np.float32).reshape(4)
 
 
