@@ -1082,9 +1082,11 @@ class TMREngine:
         H, W = (2 * Hin, 2 * Win) if self.cfg.feature_upsample else (Hin, Win)
         params = host.peak_params(boxes, H, W, cls_ths, self.cfg.box_reg, ablation_b, ablation_c)
         C = int(self.P["input_proj.0.weight"].shape[0])
-        units = host.build_units(boxes, unit_image, H, W, C, self.cfg.template_type)[0] \
-            if not self.cfg.no_matcher else np.zeros(0, UNIT_DTYPE)
-        sig = self._graph_signature(feats, units, unit_image, ablation_b, ablation_c)
+        sig = units = None
+        if self.use_graphs and len(unit_image) <= self.GRAPH_MAX_UNITS:  # else no graph prep at all
+            units = host.build_units(boxes, unit_image, H, W, C, self.cfg.template_type)[0] \
+                if not self.cfg.no_matcher else np.zeros(0, UNIT_DTYPE)
+            sig = self._graph_signature(feats, units, unit_image, ablation_b, ablation_c)
         g = self._graphs.get(sig) if sig is not None else None
         self.last_graph = "replay" if g is not None else "eager"
         if g is None and sig is not None:

@@ -32,6 +32,37 @@ def clamp_box(box) -> np.ndarray:
     return np.array([clamp01(x) for x in b], np.float32)
 
 
+def clamp01_vec(v: np.ndarray) -> np.ndarray:
+    """clamp01 elementwise with the same semantics (NaN -> 0, like Python's
+    `v if v > 0 else 0`), fp32."""
+    v = np.asarray(v, np.float32)
+    m = np.where(v > f32(0.0), v, f32(0.0)).astype(np.float32)
+    return np.where(m < f32(1.0), m, f32(1.0)).astype(np.float32)
+
+
+def template_sizes(boxes: np.ndarray, H: int, W: int):
+    """template_size over [U,4] boxes at once, the same fp32 operations per
+    element: (rois [U,4] fp32, ht [U] int, wt [U] int); raises like
+    template_size for the first box the reference would reject."""
+    c = clamp01_vec(np.asarray(boxes, np.float32).reshape(-1, 4))
+    x1, x2 = (c[:, 0] * f32(W)).astype(np.float32), (c[:, 2] * f32(W)).astype(np.float32)
+    y1, y2 = (c[:, 1] * f32(H)).astype(np.float32), (c[:, 3] * f32(H)).astype(np.float32)
+    wt = np.ceil(x2).astype(np.int64) - np.floor(x1).astype(np.int64)
+    ht = np.ceil(y2).astype(np.int64) - np.floor(y1).astype(np.int64)
+    wt -= (wt % 2 == 0)
+    ht -= (ht % 2 == 0)
+    bad = (ht <= 0) | (wt <= 0) | (ht > H) | (wt > W)
+    if bad.any():
+        template_size(np.asarray(boxes, np.float32).reshape(-1, 4)[int(np.argmax(bad))], H, W)  # raises
+    return np.stack([x1, y1, x2, y2], 1).astype(np.float32), ht, wt
+
+
+def tsplit_nk_vec(wt: np.ndarray) -> np.ndarray:
+    pw = np.asarray(wt, np.int64) // 2
+    s = ((pw + 7) & ~7) - pw
+    return np.where(16 + s + np.asarray(wt, np.int64) - 1 <= 32, 1, 2)
+
+
 def template_size(box, H: int, W: int) -> Tuple[np.ndarray, int, int]:
     """(roi in feature px, Ht, Wt) exactly as extract_template computes them
     (template_matching.py:56-73).  Raises ValueError where the reference would
@@ -86,6 +117,18 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
     U = boxes.shape[0]
     ttype = TEMPLATE_TYPES[template_type]
     units = np.zeros(U, UNIT_DTYPE)
+    if ttype == TEMPLATE_ROI_ALIGN and U:
+        # vectorised: the same fp32 arithmetic per unit as template_size
+        rois, ht, wt = template_sizes(boxes, H, W)
+        units["image"] = np.asarray(images, np.int64)[:U]
+        units["type"] = ttype
+        units["roi"] = rois
+        units["ht"], units["wt"] = ht, wt
+        sizes = C * ht * wt
+        units["tmpl_offset"] = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        rows = ht * tsplit_nk_vec(wt)
+        units["row_offset"] = np.concatenate([[0], np.cumsum(rows)[:-1]])
+        return units, int(sizes.sum()), max(1, int(ht.max())), max(1, int(wt.max()))
     off = rows = 0
     max_ht = max_wt = 1
     for u in range(U):
@@ -154,14 +197,20 @@ def peak_params(boxes: np.ndarray, H: int, W: int, cls_ths: float, box_reg: bool
     P = np.zeros(boxes.shape[0], PEAK_DTYPE)
     thr = f32(cls_ths)
     mode = 2 if not box_reg else (1 if ablation_c else 0)
-    for u, box in enumerate(boxes):
-        c = clamp_box(box)
-        bw, bh = f32(c[2] - c[0]), f32(c[3] - c[1])
-        P["thr"][u] = thr
-        P["scale_w"][u] = f32(1.0) if ablation_b else bw
-        P["scale_h"][u] = f32(1.0) if ablation_b else bh
-        P["mask"][u] = adaptive_mask(bh, bw, H, W)
-        P["mode"][u] = mode
+    # vectorised: the same fp32 arithmetic per unit as adaptive_mask
+    c = clamp01_vec(boxes)
+    bw = (c[:, 2] - c[:, 0]).astype(np.float32)
+    bh = (c[:, 3] - c[:, 1]).astype(np.float32)
+    nh, nw = 1.0 / H, 1.0 / W
+    h3, w3, h2, w2 = f32(nh * 3), f32(nw * 3), f32(nh * 2), f32(nw * 2)
+    mask = np.select([(bh >= h3) & (bw >= w3), (bh < h2) & (bw < w2), (bh < h2) & (bw >= w2),
+                      (bh >= h2) & (bw < w2)],
+                     [KERNEL_FULL, KERNEL_CENTER, KERNEL_VERT, KERNEL_HORZ], KERNEL_CROSS)
+    P["thr"] = thr
+    P["scale_w"] = f32(1.0) if ablation_b else bw
+    P["scale_h"] = f32(1.0) if ablation_b else bh
+    P["mask"] = mask
+    P["mode"] = mode
     return P
 
 

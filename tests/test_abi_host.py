@@ -284,3 +284,37 @@ def test_xcorr_cost_table_committed_crossovers(tmp_path):
     with pytest.raises(tmr_amd.TMRError, match="lacks"):
         e._load_xcorr_cost(str(part))
     assert e._load_xcorr_cost(str(tmp_path / "absent.json")) is None
+
+
+def test_build_units_vectorised_matches_scalar():
+    """host.build_units computes the ROI sizing vectorised: the same fp32
+    operations per unit as the scalar host.template_size (the reference's
+    0-d tensor math), incl. boxes on the clamp edges and NaN coordinates."""
+    H, W, C = 128, 96, 16
+    boxes = _rand_boxes(77, 500)
+    boxes = boxes[[i for i, b in enumerate(boxes) if _sizes_ok(b, H, W)]]
+    extra = np.array([[0, 0, 1, 1], [0.5, 0.5, 0.5 + 3.0 / W, 0.5 + 3.0 / H], [-0.2, 0.1, 0.3, 1.4],
+                      [np.nan, 0.2, 0.4, 0.6]], np.float32)
+    extra = extra[[i for i, b in enumerate(extra) if _sizes_ok(b, H, W)]]
+    boxes = np.concatenate([boxes, extra]).astype(np.float32)
+    ui = np.sort(np.arange(len(boxes)) % 7)
+    units, tfl, mh, mw = host.build_units(boxes, ui, H, W, C)
+    off = rows = 0
+    for u, b in enumerate(boxes):
+        roi, ht, wt = host.template_size(b, H, W)
+        assert (units["ht"][u], units["wt"][u]) == (ht, wt)
+        assert np.array_equal(units["roi"][u].view(np.uint32), roi.view(np.uint32))
+        assert units["tmpl_offset"][u] == off and units["row_offset"][u] == rows
+        off += C * ht * wt
+        rows += ht * host.tsplit_nk(wt)
+    assert tfl == off and mh == units["ht"].max() and mw == units["wt"].max()
+    with pytest.raises(ValueError):
+        host.build_units(np.array([[0.5, 0.5, 0.5, 0.5]], np.float32), [0], H, W, C)
+
+
+def _sizes_ok(b, H, W):
+    try:
+        host.template_size(b, H, W)
+        return True
+    except ValueError:
+        return False
