@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--units", type=int, default=48)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--bits", default="", help="instead: the one-term f16 kernel with weights (then "
+                    "activations) rounded to these numbers of significant bits, e.g. 11,8,6,4,2")
     a = ap.parse_args()
+    if a.bits:
+        return bits_sweep(a)
     dev = torch.device("cuda:0")
     U, C, N, H, W, ks = a.units, 512, 2048, 128, 128, 3
     g = torch.Generator(device=dev).manual_seed(0)
@@ -77,6 +81,44 @@ def main():
             print(json.dumps({"weights": wname, "data": name, "precision": a.precision, "units": U,
                               "ms": round(float(np.median(ms[1:])), 3),
                               "x_absmax": round(float(x.abs().max()), 4)}), flush=True)
+
+
+def round_bits(t: torch.Tensor, k: int) -> torch.Tensor:
+    """t rounded to k significant bits (round to nearest even by the fp32 add trick)."""
+    m, e = torch.frexp(t)
+    scale = torch.ldexp(torch.ones_like(m), torch.full_like(e, k))
+    return torch.ldexp(torch.round(m * scale) / scale, e)
+
+
+def bits_sweep(a):
+    """One fp16 MFMA term per product: does an operand with fewer significant
+    bits (fewer partial products in the multiplier) make the launch faster?"""
+    dev = torch.device("cuda:0")
+    U, C, N, H, W, ks = a.units, 512, 2048, 128, 128, 3
+    g = torch.Generator(device=dev).manual_seed(0)
+    w0 = torch.randn((N, C, ks, ks), device=dev, generator=g) * 0.01
+    x0 = torch.randn((U, C, H, W), device=dev, generator=g)
+    b = torch.zeros(N, device=dev)
+    out = torch.empty((U, N, H, W), device=dev)
+    pc = PREC_CODES["f16"]
+    for which in ("w", "x"):
+        for k in [int(v) for v in a.bits.split(",")]:
+            w = round_bits(w0, k) if which == "w" else w0
+            x = round_bits(x0, k) if which == "x" else x0
+            wp, wmax = pack_split_w(w, C, "f16")
+            xmax = absmax(x)
+            xp = pack_split_x(x, ks, "f16", xmax)
+            ms = []
+            for _ in range(a.reps + 1):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, pc, ptr(wp), ptr(wmax),
+                     ptr(xmax), ptr(b), N, 1, None, ptr(out), 0, stream())
+                e.record()
+                torch.cuda.synchronize()
+                ms.append(s.elapsed_time(e))
+            print(json.dumps({"rounded": which, "bits": k, "precision": "f16", "units": U,
+                              "ms": round(float(np.median(ms[1:])), 3)}), flush=True)
 
 
 if __name__ == "__main__":
