@@ -67,6 +67,8 @@ def variant_source(name: str, src: str) -> str:
     if name == "nodma":
         return _sub(src, "    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);",
                     "    (void)r; (void)dst; (void)voff; (void)soff;")
+    if name.startswith("wsparse"):  # weights' hi part to N significant bits (wsparse8, wsparse6)
+        return _sub(src, "constexpr int WH_BITS = 11;", f"constexpr int WH_BITS = {int(name[7:])};")
     if name == "l2dma":
         src = _sub(src, "        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;",
                    "        const uint32_t soff = 0u * (uint32_t)(s0 ? hc : hc - h0) * cstride;")

@@ -172,6 +172,41 @@ __device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
         }
 }
 
+// Weight split of the F16X3 records: w s = wh + wl with wh = w s rounded to
+// WH_BITS significant bits (fp32 round-to-nearest-even on the bit pattern,
+// then exact in fp16) and wl = fp16(w s - wh).  WH_BITS = 11 is the plain
+// fp16 hi/lo split (wh = fp16(w s)).
+constexpr int WH_BITS = 11;
+
+__device__ __forceinline__ float round_sig_bits(float f, int bits) {
+    uint32_t u = __float_as_uint(f);
+    const uint32_t drop = 24u - (uint32_t)bits;
+    if (drop == 0u || (u & 0x7f800000u) == 0x7f800000u) return f;
+    const uint32_t half = 1u << (drop - 1u);
+    u = (u + half - 1u + ((u >> drop) & 1u)) & ~((1u << drop) - 1u);
+    return __uint_as_float(u);
+}
+
+template <int PREC>
+__device__ __forceinline__ void split_record_w(const float (&v)[CCH], float s,
+                                               typename Prec<PREC>::V (&hi)[P],
+                                               typename Prec<PREC>::V (&lo)[P]) {
+    typedef typename Prec<PREC>::E E;
+    if constexpr (Prec<PREC>::HALVES != 2 || WH_BITS >= 11) {
+        split_record<PREC>(v, s, hi, lo);
+    } else {
+#pragma unroll
+        for (int g = 0; g < P; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float xs = v[g * 8 + j] * s;
+                const E h = (E)round_sig_bits(xs, WH_BITS);
+                hi[g][j] = h;
+                lo[g][j] = (E)(xs - (float)h);
+            }
+    }
+}
+
 struct SArgs {
     const char *x0;   // packed src0 [img][NC0*HALVES][Hp][Wp][64 B]
     const char *x1;   // packed src1 [u][NC1*HALVES][Hp][Wp][64 B]
@@ -1003,7 +1038,7 @@ __global__ void wpack_kernel(const float *__restrict__ w, int N, int C0, int C1,
         v[k] = (ok && n < N) ? w[((size_t)n * C + ch) * T + tap] : 0.0f;
     }
     typename Prec<PREC>::V hi[P], lo[P];
-    split_record<PREC>(v, sc, hi, lo);
+    split_record_w<PREC>(v, sc, hi, lo);
     // planar: [tap][chunk][plane (wh pieces, then wl pieces)][Npad] 16-B pieces
     constexpr int NP = Prec<PREC>::WREC / 16;
     typename Prec<PREC>::V *o = out + ((size_t)tap * NC + c) * NP * Npad + n;
