@@ -174,9 +174,16 @@ __device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
 
 // Weight split of the F16X3 records: w s = wh + wl with wh = w s rounded to
 // WH_BITS significant bits (fp32 round-to-nearest-even on the bit pattern,
-// then exact in fp16) and wl = fp16(w s - wh).  WH_BITS = 11 is the plain
-// fp16 hi/lo split (wh = fp16(w s)).
-constexpr int WH_BITS = 11;
+// then exact in fp16) and wl = fp16(w s - wh); WH_BITS = 11 would be the
+// plain fp16 hi/lo split (wh = fp16(w s)).  The decoder is power-bound and
+// its MFMA rate rises as the operands' bit density falls:
+// wh with 6 significant bits feeds two of the three MFMAs per product.  The
+// weights keep 6 + 11 = 17 bits, the dropped wl xl term is ~2^-17 of a
+// product.  Measured (profiles/r04j, A/B in one call): heads launch 111.6 /
+// 111.7 -> 108.3 / 108.5 ms (config B 448.0 / 446.4 -> 459.3 / 458.0
+// images/s; 8 bits: 109.9 ms); decoder-conv normwise error vs fp64 2.1e-6 ->
+// 3.0e-6 (contract 1e-5).
+constexpr int WH_BITS = 6;
 
 __device__ __forceinline__ float round_sig_bits(float f, int bits) {
     uint32_t u = __float_as_uint(f);
