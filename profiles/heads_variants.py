@@ -12,6 +12,8 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
   noacc0   no initial-value (acc0) read: accumulators start at zero
   noepi    no heads epilogue: one dummy store per block
   nodma    no LDS-DMA at all (halo and weights never loaded)
+  wsparseN / tsparseN   decoder weights' / correlation templates' hi part at
+           N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   l2dma    every DMA re-reads the first chunk's halo / first step's weights:
            the same instruction stream with real operand data, but L2-resident
            (no MALL / HBM traffic)
@@ -21,6 +23,7 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
     python profiles/heads_variants.py clean
 """
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -67,8 +70,10 @@ def variant_source(name: str, src: str) -> str:
     if name == "nodma":
         return _sub(src, "    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);",
                     "    (void)r; (void)dst; (void)voff; (void)soff;")
-    if name.startswith("wsparse"):  # weights' hi part to N significant bits (wsparse8, wsparse6)
-        return _sub(src, "constexpr int WH_BITS = 11;", f"constexpr int WH_BITS = {int(name[7:])};")
+    if name.startswith("wsparse"):  # weights' hi part to N significant bits (wsparse8, wsparse11)
+        return re.sub(r"constexpr int WH_BITS = \d+;", f"constexpr int WH_BITS = {int(name[7:])};", src, count=1)
+    if name.startswith("tsparse"):  # correlation templates' hi part (xcorr.hip TH_BITS)
+        return _sub(src, "constexpr int TH_BITS = 11;", f"constexpr int TH_BITS = {int(name[7:])};")
     if name == "l2dma":
         src = _sub(src, "        const uint32_t soff = (uint32_t)(s0 ? hc : hc - h0) * cstride;",
                    "        const uint32_t soff = 0u * (uint32_t)(s0 ? hc : hc - h0) * cstride;")
@@ -78,6 +83,10 @@ def variant_source(name: str, src: str) -> str:
                    "const uint32_t src = (uint32_t)tl * tapstride + wnt +")
         return src
     raise SystemExit(f"unknown variant {name}")
+
+
+def variant_file(name: str) -> str:
+    return "xcorr.hip" if name.startswith("tsparse") else "conv_split.hip"
 
 
 VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma", "l2dma"]
@@ -99,7 +108,7 @@ def build(names, rev_file=None):
                     txt = subprocess.run(["git", "-C", REPO, "show", f"{rev_file[0]}:{rel}"], check=True,
                                          capture_output=True, text=True).stdout
                     txt = txt.replace("../../include/", "../../../include/")
-                elif rev_file is None and f == "conv_split.hip":
+                elif rev_file is None and f == variant_file(name):
                     txt = variant_source(name, txt)
                 with open(p, "w") as fh:
                     fh.write(txt)

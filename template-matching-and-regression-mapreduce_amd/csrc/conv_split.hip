@@ -185,15 +185,6 @@ __device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
 // 3.0e-6 (contract 1e-5).
 constexpr int WH_BITS = 6;
 
-__device__ __forceinline__ float round_sig_bits(float f, int bits) {
-    uint32_t u = __float_as_uint(f);
-    const uint32_t drop = 24u - (uint32_t)bits;
-    if (drop == 0u || (u & 0x7f800000u) == 0x7f800000u) return f;
-    const uint32_t half = 1u << (drop - 1u);
-    u = (u + half - 1u + ((u >> drop) & 1u)) & ~((1u << drop) - 1u);
-    return __uint_as_float(u);
-}
-
 template <int PREC>
 __device__ __forceinline__ void split_record_w(const float (&v)[CCH], float s,
                                                typename Prec<PREC>::V (&hi)[P],
@@ -207,7 +198,7 @@ __device__ __forceinline__ void split_record_w(const float (&v)[CCH], float s,
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float xs = v[g * 8 + j] * s;
-                const E h = (E)round_sig_bits(xs, WH_BITS);
+                const E h = (E)tmr_round_sig_bits(xs, WH_BITS);
                 hi[g][j] = h;
                 lo[g][j] = (E)(xs - (float)h);
             }

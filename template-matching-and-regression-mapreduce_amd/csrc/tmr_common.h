@@ -47,6 +47,18 @@ static inline hipError_t tmr_set_max_lds(const void *fn, size_t bytes) {
 // The reference's torch.exp / torch.sigmoid bits depend on the backend and on
 // the element's position (vector body vs scalar tail on CPU); the path's
 // decode contract is defined on these ("bit-exactness").
+// f rounded to `bits` significant bits (round to nearest even on the fp32 bit
+// pattern; inf/NaN unchanged): the sparse hi part of the 3-term split records
+// (conv_split.hip WH_BITS, xcorr.hip TH_BITS)
+__device__ __forceinline__ float tmr_round_sig_bits(float f, int bits) {
+    uint32_t u = __float_as_uint(f);
+    const uint32_t drop = 24u - (uint32_t)bits;
+    if (drop == 0u || (u & 0x7f800000u) == 0x7f800000u) return f;
+    const uint32_t half = 1u << (drop - 1u);
+    u = (u + half - 1u + ((u >> drop) & 1u)) & ~((1u << drop) - 1u);
+    return __uint_as_float(u);
+}
+
 __device__ __forceinline__ float tmr_expf_cr(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float tmr_sigmoid_cr(float x) {
     return (float)(1.0 / (1.0 + exp(-(double)x)));

@@ -589,6 +589,13 @@ __device__ __forceinline__ float block_max(float v, float *red) {
 // One wave per (unit, channel).
 constexpr int AFRAG = 64 * 16;  // bytes per (row, nk, term) fragment
 
+// Template split of the 3-term fragments: t 2^-e = th + tl with th rounded to
+// TH_BITS significant bits (exact in fp16) and tl = fp16(t 2^-e - th), the
+// correlation's counterpart of conv_split.hip's WH_BITS (th feeds two of the
+// three MFMAs per product; fewer set bits, less MFMA power).  11 = the plain
+// fp16 hi/lo split.
+constexpr int TH_BITS = 11;
+
 __host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per template row
     const int pw = w / 2, s = ((pw + 7) & ~7) - pw;
     return 16 + s + w - 1 <= 32 ? 1 : 2;
@@ -646,7 +653,8 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 h8 hi, lo;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    hi[q] = (_Float16)x[q];
+                    // 3-term: sparse hi (TH_BITS); one-term f16 reads the plain fp16 hi
+                    hi[q] = (lo_too && TH_BITS < 11) ? (_Float16)tmr_round_sig_bits(x[q], TH_BITS) : (_Float16)x[q];
                     lo[q] = (_Float16)(x[q] - (float)hi[q]);
                 }
                 *reinterpret_cast<h8 *>(f) = hi;
