@@ -593,7 +593,10 @@ constexpr int AFRAG = 64 * 16;  // bytes per (row, nk, term) fragment
 // TH_BITS significant bits (exact in fp16) and tl = fp16(t 2^-e - th), the
 // correlation's counterpart of conv_split.hip's WH_BITS (th feeds two of the
 // three MFMAs per product; fewer set bits, less MFMA power).  11 = the plain
-// fp16 hi/lo split.
+// fp16 hi/lo split, kept: unlike the decoder (busy 0.83, power-bound) this
+// kernel gains nothing measurable (profiles/r04k, A/B in one call: config-E
+// mix 12.21 / 12.19 -> 12.14 / 12.12 ms at 6 bits, config-B mix 4.49 / 4.51
+// -> 4.47 / 4.51) for a 2-5x larger error (4e-7..1.5e-6 -> 1.1e-6..2.3e-6).
 constexpr int TH_BITS = 11;
 
 __host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per template row
