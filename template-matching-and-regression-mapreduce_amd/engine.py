@@ -347,13 +347,21 @@ class _DetectGraph:
 
     def __init__(self, graph, feats, slots, outputs, last):
         self.graph, self.feats, self.slots, self.outputs, self.last = graph, feats, slots, outputs, last
+        self.done = None  # event after the last replay: its copy nodes read the pinned slots
 
     def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray]):
+        # the slots are rewritten by the host at once: a previous replay still
+        # queued (two calls with no sync between them) must have read them first
+        if self.done is not None:
+            self.done.synchronize()
         for tag, arr in host.items():
             dst = self.slots[tag].numpy()
             np.copyto(dst, np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
         self.feats.copy_(feats)
         self.graph.replay()
+        if self.done is None:
+            self.done = torch.cuda.Event()
+        self.done.record()
         return self.outputs
 
 

@@ -411,3 +411,32 @@ def test_module_graph_replay_matches_eager():
         assert bits_equal(kept[0][0][0].cpu().numpy(), again[0][0].cpu().numpy())
         assert bits_equal(kept[0][2][0].cpu().numpy(), again[2][0].cpu().numpy())
     assert "replay" in modes and "captured" in modes, (modes, model.engine().last_graph_error)
+
+
+def test_module_graph_replays_back_to_back():
+    """Replays queued with no host sync between them (a caller that runs every
+    exemplar's forward before reading any result): each replay rewrites the
+    graph's pinned host-input slots, so it must not do so before the previous
+    replay's copies have read them.  Every output equals the eager engine's."""
+    args, model, P, feats0, ex0 = _model_and_inputs(seed=37, E=3, hf=16, cin=32, emb=48)
+    _, ref_model, _, _, _ = _model_and_inputs(seed=37, E=3, hf=16, cin=32, emb=48)
+    ref_model.engine().use_graphs = False
+    calls = []
+    for img in range(5):
+        feats = cuda(synth.sam_features(80 + img, 1, 32, 16, 16))
+        ex = ex0.copy()
+        ex[..., [0, 2]] += 0.004 * img
+        ex[..., [1, 3]] -= 0.002 * img
+        calls += [(feats, [e.unsqueeze(0)]) for e in cuda(ex[0])]
+    with torch.no_grad():
+        for f, e in calls:  # first sightings: the graphs are captured (synced)
+            model(f, e)[0][0].cpu()
+        outs, modes = [], []
+        for f, e in calls:  # no sync in between
+            outs.append(model(f, e))
+            modes.append(model.engine().last_graph)
+        for (f, e), out in zip(calls, outs):
+            want = ref_model(f, e)
+            for g_, w_ in zip(out[:3], want[:3]):
+                assert bits_equal(g_[0].cpu().numpy(), w_[0].cpu().numpy())
+    assert modes.count("replay") >= len(calls) - 2, (modes, model.engine().last_graph_error)
