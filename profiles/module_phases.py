@@ -48,6 +48,7 @@ class _Counts:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--cprofile", default="", help="write a cProfile of the timed steps to this file")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from types import SimpleNamespace
@@ -89,11 +90,12 @@ def main():
 
     def image(b):
         stamp("img")
+        image_t = feats[0:1]  # a fresh view per image, as bench.py's loop makes
         ex_d = torch.from_numpy(ex[0]).pin_memory().to(dev, non_blocking=True)
         pl, pb, pr = [], [], []
         for exemplar in [[ex_d[e].unsqueeze(0)] for e in range(E)]:
             stamp("fwd")
-            po, preg, _, _ = model(feats, exemplar)
+            po, preg, _, _ = model(image_t, exemplar)
             stamp("gpb")
             _l, _b, _r = tmr.Get_pred_boxes(po, preg, exemplar, dummy, 0.7, True)
             stamp("gpb1")
@@ -108,11 +110,21 @@ def main():
             image(b)
         torch.cuda.synchronize()
         STAMPS.clear()
+        prof = None
+        if a.cprofile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for b in range(B):
             image(b)
         torch.cuda.synchronize()
         total = time.perf_counter() - t0
+        if prof is not None:
+            prof.disable()
+            import pstats
+            with open(a.cprofile, "w") as fh:
+                pstats.Stats(prof, stream=fh).sort_stats("tottime").print_stats(45)
     # intervals between consecutive stamps, by (from, to) tag pair
     agg = {}
     for (t1, a1), (t2, a2) in zip(STAMPS, STAMPS[1:]):

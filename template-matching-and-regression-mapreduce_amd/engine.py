@@ -348,6 +348,7 @@ class _DetectGraph:
     def __init__(self, graph, feats, slots, outputs, last):
         self.graph, self.feats, self.slots, self.outputs, self.last = graph, feats, slots, outputs, last
         self.done = None  # event after the last replay: its copy nodes read the pinned slots
+        self.src = None  # (tensor ref, version, data_ptr) of the features last copied into feats
 
     def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray]):
         # the slots are rewritten by the host at once: a previous replay still
@@ -357,7 +358,10 @@ class _DetectGraph:
         for tag, arr in host.items():
             dst = self.slots[tag].numpy()
             np.copyto(dst, np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
-        self.feats.copy_(feats)
+        src = self.src
+        if src is None or src[0]() is not feats or src[1] != (feats._version, feats.data_ptr()):
+            self.feats.copy_(feats)  # (the module API's later exemplars reuse the image's copy)
+            self.src = (weakref.ref(feats), (feats._version, feats.data_ptr()))
         self.graph.replay()
         if self.done is None:
             self.done = torch.cuda.Event()
@@ -984,8 +988,11 @@ class TMREngine:
             unit_off: torch.Tensor, seg_units: np.ndarray, iou_threshold: float,
             want_keep: bool = False):
         """Greedy NMS per image over its units' candidates (+ dummy rows).
-        Returns per-image lists of (logits, boxes, refs) device tensors
-        (+ keep indices when want_keep)."""
+        counts: the device counts, or None (staged from counts_host);
+        unit_off: a device tensor or a host int64 array (staged).  The host
+        arrays go to the device as ONE staged copy (this runs right after the
+        counts sync, while the GPU idles).  Returns per-image lists of
+        (logits, boxes, refs) device tensors (+ keep indices when want_keep)."""
         dev = logits.device
         G = len(seg_units) - 1
         cand_off, nb_off, max_cand = host.nms_offsets(counts_host, seg_units)
@@ -993,9 +1000,28 @@ class TMREngine:
         sum_nb = int(nb_off[-1])
         work = torch.empty(max(load().tmr_nms_work_size(T, sum_nb, max_cand, G), 1), device=dev,
                            dtype=torch.uint8)
-        seg_d = _h2d(np.asarray(seg_units, np.int32), dev)
-        coff_d = _h2d(np.asarray(cand_off), dev)
-        nboff_d = _h2d(np.asarray(nb_off), dev)
+        parts = [np.asarray(seg_units, np.int32), np.asarray(cand_off, np.int64), np.asarray(nb_off, np.int64)]
+        if counts is None:
+            parts.append(np.asarray(counts_host, np.int32))
+        host_off = not isinstance(unit_off, torch.Tensor)
+        if host_off:
+            parts.append(np.asarray(unit_off, np.int64))
+        offs, o = [], 0
+        for a in parts:  # 8-B aligned sections of one byte blob
+            offs.append(o)
+            o += (a.nbytes + 7) // 8 * 8
+        blob = np.zeros(max(o, 8), np.uint8)
+        for a, q in zip(parts, offs):
+            blob[q:q + a.nbytes] = a.view(np.uint8)
+        blob_d = _h2d(blob, dev)
+        views = [blob_d[q:q + a.nbytes].view(torch.int32 if a.dtype == np.int32 else torch.int64)
+                 for a, q in zip(parts, offs)]
+        seg_d, coff_d, nboff_d = views[:3]
+        rest = views[3:]
+        if counts is None:
+            counts = rest.pop(0)
+        if host_off:
+            unit_off = rest.pop(0)
         out_l = torch.empty((T, 2), device=dev, dtype=torch.float32)
         out_b = torch.empty((T, 4), device=dev, dtype=torch.float32)
         out_r = torch.empty((T, 2), device=dev, dtype=torch.float32)
@@ -1116,6 +1142,6 @@ class TMREngine:
             logits, box, ref, counts = self._forward_peaks(feats, unit_image, boxes, params)
         counts_host = counts.cpu().numpy()  # torch.where-style sync (TM_utils.py:254)
         U = B * E
-        unit_off = torch.arange(U, device=feats.device, dtype=torch.int64) * (H * W)
+        unit_off = np.arange(U, dtype=np.int64) * (H * W)  # staged by nms with its other host arrays
         seg = np.arange(0, U + 1, E, dtype=np.int64)
         return self.nms(logits, box, ref, counts, counts_host, unit_off, seg, iou_threshold)

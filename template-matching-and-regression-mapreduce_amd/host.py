@@ -32,6 +32,15 @@ def clamp_box(box) -> np.ndarray:
     return np.array([clamp01(x) for x in b], np.float32)
 
 
+_F0, _F1 = f32(0.0), f32(1.0)
+
+
+def _clamp01_fast(v: np.float32) -> np.float32:
+    """clamp01 of an fp32 scalar (no conversions: the per-unit path)."""
+    m = v if v > _F0 else _F0
+    return m if m < _F1 else _F1
+
+
 def clamp01_vec(v: np.ndarray) -> np.ndarray:
     """clamp01 elementwise with the same semantics (NaN -> 0, like Python's
     `v if v > 0 else 0`), fp32."""
@@ -67,9 +76,12 @@ def template_size(box, H: int, W: int) -> Tuple[np.ndarray, int, int]:
     """(roi in feature px, Ht, Wt) exactly as extract_template computes them
     (template_matching.py:56-73).  Raises ValueError where the reference would
     ask roi_align for a non-positive output size."""
-    c = clamp_box(box)
-    x1, x2 = f32(c[0] * f32(W)), f32(c[2] * f32(W))
-    y1, y2 = f32(c[1] * f32(H)), f32(c[3] * f32(H))
+    b = box if isinstance(box, np.ndarray) and box.dtype == np.float32 and box.shape == (4,) else \
+        np.asarray(box, dtype=np.float32).reshape(4)
+    c0, c1, c2, c3 = (_clamp01_fast(v) for v in b)
+    fW, fH = f32(W), f32(H)
+    x1, x2 = c0 * fW, c2 * fW  # fp32 scalar products (np.float32 * np.float32)
+    y1, y2 = c1 * fH, c3 * fH
     wt = math.ceil(float(x2)) - math.floor(float(x1))
     ht = math.ceil(float(y2)) - math.floor(float(y1))
     if wt % 2 == 0:
@@ -110,6 +122,9 @@ def tsplit_rows(units: np.ndarray) -> int:
     return int(sum(int(h) * tsplit_nk(int(w)) for h, w in zip(units["ht"], units["wt"])))
 
 
+SMALL_UNITS = 8  # up to this many units build_units runs per unit
+
+
 def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int,
                 template_type: str = "roi_align"):
     """tmr_unit_t array for U units.  Returns (units, template_floats, max_ht, max_wt)."""
@@ -117,7 +132,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
     U = boxes.shape[0]
     ttype = TEMPLATE_TYPES[template_type]
     units = np.zeros(U, UNIT_DTYPE)
-    if ttype == TEMPLATE_ROI_ALIGN and U:
+    if ttype == TEMPLATE_ROI_ALIGN and U > SMALL_UNITS:
         # vectorised: the same fp32 arithmetic per unit as template_size
         rois, ht, wt = template_sizes(boxes, H, W)
         units["image"] = np.asarray(images, np.int64)[:U]
@@ -129,21 +144,19 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         rows = ht * tsplit_nk_vec(wt)
         units["row_offset"] = np.concatenate([[0], np.cumsum(rows)[:-1]])
         return units, int(sizes.sum()), max(1, int(ht.max())), max(1, int(wt.max()))
+    # per unit (prototype templates, and few units: the module API's one
+    # exemplar per call, where the vector form's per-call overhead dominates)
     off = rows = 0
     max_ht = max_wt = 1
+    zero4 = (0, 0, 0, 0)
     for u in range(U):
-        units["image"][u] = int(images[u])
-        units["type"][u] = ttype
         if ttype == TEMPLATE_ROI_ALIGN:
             roi, ht, wt = template_size(boxes[u], H, W)
-            units["roi"][u] = roi
+            roi, pbox = tuple(roi.tolist()), zero4
         else:
-            units["pbox"][u] = prototype_box(boxes[u], H, W)
-            ht = wt = 1
-        units["ht"][u] = ht
-        units["wt"][u] = wt
-        units["tmpl_offset"][u] = off
-        units["row_offset"][u] = rows
+            pbox = tuple(prototype_box(boxes[u], H, W).tolist())
+            roi, ht, wt = (0.0, 0.0, 0.0, 0.0), 1, 1
+        units[u] = (int(images[u]), ttype, ht, wt, roi, pbox, off, rows)
         off += C * ht * wt
         rows += ht * tsplit_nk(wt)
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
@@ -152,6 +165,17 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
 
 def image_ranges(unit_image: Sequence[int], B: int) -> np.ndarray:
     """[B+1] int32 unit ranges per image; units must be sorted by image."""
+    if len(unit_image) <= SMALL_UNITS:  # per unit (the module API's calls)
+        r, prev = [0] * (B + 1), 0
+        for i in unit_image:
+            i = int(i)
+            if i < prev or i < 0 or i >= B:
+                raise ValueError("units must be sorted by image and index images of the batch")
+            prev = i
+            r[i + 1] += 1
+        for b in range(B):
+            r[b + 1] += r[b]
+        return np.array(r, np.int32)
     ui = np.asarray(unit_image, np.int64)
     if len(ui) and (np.any(np.diff(ui) < 0) or ui.min() < 0 or ui.max() >= B):
         raise ValueError("units must be sorted by image and index images of the batch")

@@ -63,9 +63,35 @@ class matching_net(nn.Module):
         self.ltrbs_head = BboxesHead(self.decoder_b.out_channels) if self.box_reg else None
         self._engine = None
 
+    def _param_slots(self):
+        """(edges, slots) of the module tree: edges (parent, name, child) of
+        every registered submodule and each module's parameter count; slots
+        (key, module, name) of every parameter outside the encoder.  Built by
+        one walk, reused while every edge and count still holds (a submodule
+        or parameter added or replaced re-runs the walk)."""
+        c = getattr(self, "_pslots", None)
+        if c is not None and all(p._modules.get(n) is m for p, n, m in c[0]) and \
+                all(len(m._parameters) == k for m, k in c[1]):
+            return c[2]
+        edges, counts, slots = [], [], []
+        for pre, m in self.named_modules():
+            counts.append((m, len(m._parameters)))
+            for n, ch in m._modules.items():
+                if ch is not None:
+                    edges.append((m, n, ch))
+            if pre == "encoder" or pre.startswith("encoder."):
+                continue
+            for n, v in m._parameters.items():
+                if v is not None:
+                    slots.append((f"{pre}.{n}" if pre else n, m, n))
+        object.__setattr__(self, "_pslots", (edges, counts, slots))
+        return slots
+
     def path_params(self):
-        """The hot-path parameters under their reference state_dict keys."""
-        P = {k: v for k, v in self.named_parameters() if not k.startswith("encoder.")}
+        """The hot-path parameters under their reference state_dict keys
+        (the parameters read through their slots: a parameter re-bound by
+        to() / load_state_dict(assign=True) / setattr is the one returned)."""
+        P = {k: m._parameters[n] for k, m, n in self._param_slots()}
         if self.matcher is None:
             P["matcher.scale"] = torch.ones(1, device=P["input_proj.0.weight"].device)
         return P

@@ -12,7 +12,7 @@ import torch
 
 from . import host
 from ._lib import TMRError, call, ptr, require_gpu, stream
-from .engine import TMREngine, _h2d
+from .engine import TMREngine
 from .template_matching import _box_host
 
 
@@ -63,10 +63,20 @@ def adaptive_kernel_generater(ex_size, pred_size):
     return host.mask_to_kernel(host.adaptive_mask(ex_h, ex_w, int(pred_size[0]), int(pred_size[1])))
 
 
+_DUMMY: "dict[tuple, tuple]" = {}
+
+
 def _dummy(dtype, device):
-    return (torch.tensor([[0.0, 0.0]], dtype=dtype, device=device),
-            torch.tensor([[0.0, 0.0, 1e-14, 1e-14]], dtype=dtype, device=device),
-            torch.tensor([[0.0, 0.0]], dtype=dtype, device=device))
+    """The empty-unit rows of TM_utils.py:288-291, fresh tensors per call.
+    Cloned on the device from a cached copy: building them from Python
+    values is a pageable host->device copy, which waits for the stream."""
+    key = (dtype, str(device))
+    d = _DUMMY.get(key)
+    if d is None:
+        d = _DUMMY[key] = (torch.tensor([[0.0, 0.0]], dtype=dtype, device=device),
+                           torch.tensor([[0.0, 0.0, 1e-14, 1e-14]], dtype=dtype, device=device),
+                           torch.tensor([[0.0, 0.0]], dtype=dtype, device=device))
+    return tuple(t.clone() for t in d)
 
 
 def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=0.1, box_reg=True,
@@ -117,16 +127,20 @@ def _nms_lists(pred_logits, pred_boxes, ref_points, iou_threshold, want_keep=Fal
         dev = pred_logits[live[0]].device
         for g in live:
             require_gpu(pred_logits[g], "pred_logits")
-        lg = torch.cat([pred_logits[g].float() for g in live]).contiguous()
-        bx = torch.cat([pred_boxes[g].float() for g in live]).contiguous()
-        rf = torch.cat([ref_points[g].float() for g in live]).contiguous()
+        if len(live) == 1:  # one list (the demo.py call form): no concatenation copy
+            g0 = live[0]
+            lg, bx, rf = (pred_logits[g0].float().contiguous(), pred_boxes[g0].float().contiguous(),
+                          ref_points[g0].float().contiguous())
+        else:
+            lg = torch.cat([pred_logits[g].float() for g in live]).contiguous()
+            bx = torch.cat([pred_boxes[g].float() for g in live]).contiguous()
+            rf = torch.cat([ref_points[g].float() for g in live]).contiguous()
         counts_h = ns[live]
         unit_off = np.zeros(len(live), np.int64)
         unit_off[1:] = np.cumsum(counts_h)[:-1]
-        counts = _h2d(counts_h.astype(np.int32), dev)  # staged, no stream sync
         seg = np.arange(len(live) + 1, dtype=np.int64)
-        r = TMREngine.nms(lg, bx, rf, counts, counts_h, _h2d(unit_off, dev), seg,
-                          iou_threshold, want_keep=want_keep)
+        # counts and unit offsets staged by nms in its one host->device copy
+        r = TMREngine.nms(lg, bx, rf, None, counts_h, unit_off, seg, iou_threshold, want_keep=want_keep)
         for i, g in enumerate(live):
             outs[g] = tuple(x[i] for x in r)
     return outs

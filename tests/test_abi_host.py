@@ -310,6 +310,25 @@ def test_build_units_vectorised_matches_scalar():
     assert tfl == off and mh == units["ht"].max() and mw == units["wt"].max()
     with pytest.raises(ValueError):
         host.build_units(np.array([[0.5, 0.5, 0.5, 0.5]], np.float32), [0], H, W, C)
+    # up to host.SMALL_UNITS units the builder runs per unit: the same records
+    assert len(boxes) > host.SMALL_UNITS
+    u0 = 0
+    for n in list(range(1, host.SMALL_UNITS + 1)) * 8:
+        if u0 + n > len(boxes):
+            break
+        small, tfl_s, mh_s, mw_s = host.build_units(boxes[u0:u0 + n], ui[u0:u0 + n], H, W, C)
+        ref = units[u0:u0 + n].copy()
+        ref["tmpl_offset"] -= ref["tmpl_offset"][0]
+        ref["row_offset"] -= ref["row_offset"][0]
+        for f in small.dtype.names:  # field-wise (a structured copy leaves the padding undefined)
+            a, b = np.ascontiguousarray(small[f]), np.ascontiguousarray(ref[f])
+            assert a.tobytes() == b.tobytes(), (u0, n, f)
+        assert (mh_s, mw_s) == (max(1, ref["ht"].max()), max(1, ref["wt"].max()))
+        assert tfl_s == int((C * ref["ht"].astype(np.int64) * ref["wt"]).sum())
+        u0 += n
+    with pytest.raises(ValueError):
+        host.build_units(np.array([[0.5, 0.5, 0.5, 0.5]] * (host.SMALL_UNITS + 1), np.float32),
+                         [0] * (host.SMALL_UNITS + 1), H, W, C)
 
 
 def _sizes_ok(b, H, W):
@@ -318,3 +337,21 @@ def _sizes_ok(b, H, W):
         return True
     except ValueError:
         return False
+
+
+def test_image_ranges_small_and_vector_forms_agree():
+    """host.image_ranges runs per unit up to host.SMALL_UNITS units and
+    vectorised above: the same [B+1] ranges, the same refusals."""
+    rng = np.random.default_rng(5)
+    for U in list(range(0, 2 * host.SMALL_UNITS + 2)):
+        B = int(rng.integers(1, 6))
+        ui = np.sort(rng.integers(0, B, U))
+        want = np.zeros(B + 1, np.int64)
+        for i in ui:
+            want[i + 1:] += 1
+        got = host.image_ranges(ui, B)
+        assert got.dtype == np.int32 and np.array_equal(got, want), (U, B)
+    for bad in ([1, 0], [0, 3], [-1, 0]):
+        for pad in (0, host.SMALL_UNITS):
+            with pytest.raises(ValueError):
+                host.image_ranges([0] * pad + bad if bad[0] >= 0 else bad + [0] * pad, 3)
