@@ -268,7 +268,9 @@ int tmr_maxpool3x3(const float *x, int64_t planes, int H, int W, int mask9, floa
  * itself when input_is_prob), masked 3x3 local max with zero padding,
  * p >= thr, row-major compaction (no cap), decode.  Outputs per unit u at
  * stride cap = H*W: logits[(u*cap+i)*2] = (p, 0) (TM_utils.py:260-261),
- * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u].
+ * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u]; a unit
+ * with no peak (counts[u] = 0) gets the reference's dummy row at its row 0
+ * (logits (0,0), box (0,0,1e-14,1e-14), ref (0,0); TM_utils.py:288-291).
  * prob [U,H,W] receives the probability map (required).
  * exp_table (device, nullable): the reference-exp table (tmr_amd/exp_table.py:
  * 128-B header, uint32 offsets[65537], sorted uint16 low halves).  The decode's

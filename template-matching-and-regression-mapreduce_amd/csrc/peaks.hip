@@ -127,9 +127,16 @@ __global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ pro
         total += s;
     }
     int pos = wbase + incl - cnt;
-    if (threadIdx.x == 0) counts[u] = total;
-    if (cnt == 0) return;
     const size_t cap = (size_t)HW;
+    if (threadIdx.x == 0) {
+        counts[u] = total;
+        if (total == 0) {  // the empty unit's dummy row (TM_utils.py:288-291) at row 0
+            *reinterpret_cast<float2 *>(logits + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
+            *reinterpret_cast<float4 *>(box + (size_t)u * cap * 4) = float4{0.0f, 0.0f, 1e-14f, 1e-14f};
+            *reinterpret_cast<float2 *>(ref + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
+        }
+    }
+    if (cnt == 0) return;
     const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
     for (int i = beg; i < end; ++i) {
         const int y = i / W, x = i % W;

@@ -104,6 +104,9 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         cap = H * W
         per_level.append([(logits[b * cap:b * cap + counts[b]], box[b * cap:b * cap + counts[b]],
                            ref[b * cap:b * cap + counts[b]]) for b in range(B)])
+        if level == 0:  # an empty unit's row 0 holds the dummy row (tmr_peaks_decode)
+            dummies = [(logits[b * cap:b * cap + 1], box[b * cap:b * cap + 1], ref[b * cap:b * cap + 1])
+                       for b in range(B)]
     pred_logits, pred_boxes, ref_points = [], [], []
     for b in range(B):
         parts = [lv[b] for lv in per_level]
@@ -112,8 +115,8 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         else:
             lg = torch.cat([p[0] for p in parts]); bx = torch.cat([p[1] for p in parts])
             rf = torch.cat([p[2] for p in parts])
-        if lg.shape[0] == 0:
-            lg, bx, rf = _dummy(dtype, device)
+        if lg.shape[0] == 0:  # every level empty: the dummy row
+            lg, bx, rf = dummies[b] if dtype == torch.float32 else _dummy(dtype, device)
         pred_logits.append(lg); pred_boxes.append(bx); ref_points.append(rf)
     return pred_logits, pred_boxes, ref_points
 

@@ -538,6 +538,31 @@ def test_get_pred_boxes_golden(golden):
             assert bits_equal(bx, oB[b]), (i, b)
 
 
+def test_get_pred_boxes_empty_units_dummy_row():
+    """A unit with no peak returns the reference's dummy row (TM_utils.py:
+    288-291), which tmr_peaks_decode writes at the unit's row 0: values and
+    shapes equal the oracle's, next to non-empty units, twice in a row (the
+    row of a unit that had peaks the call before is rewritten)."""
+    H = W = 32
+    prob = np.full((3, H, W), 0.05, np.float32)
+    prob[1, 10, 12] = 0.9  # unit 1 has one peak, units 0 and 2 none
+    reg = synth.normal(91, (3, 4, H, W)) * 0.5
+    ex = np.array([[0.1, 0.1, 0.3, 0.3], [0.2, 0.2, 0.5, 0.6], [0.4, 0.1, 0.6, 0.2]], np.float32)
+    batch = {"regression_ablation_b": False, "regression_ablation_c": False}
+    for order in ((0, 1, 2), (1, 0, 2)):
+        p_, r_, e_ = prob[list(order)], reg[list(order)], ex[list(order)]
+        L, Bx, R = tmr_amd.Get_pred_boxes([cuda(p_[:, None])], [cuda(r_)], [cuda(e[None]) for e in e_], batch,
+                                          0.5, True, input_is_prob=True)
+        oL, oB, oR = oracle.get_pred_boxes_prob(list(p_), list(r_), [e[None] for e in e_], 0.5, True, False, False)
+        for b in range(3):
+            assert L[b].dtype == torch.float32 and tuple(L[b].shape) == np.asarray(oL[b]).shape
+            assert bits_equal(L[b].cpu().numpy(), oL[b]) and bits_equal(Bx[b].cpu().numpy(), oB[b])
+            assert bits_equal(R[b].cpu().numpy(), oR[b])
+        empty = [b for b in range(3) if order[b] != 1]
+        for b in empty:
+            assert np.array_equal(Bx[b].cpu().numpy(), np.array([[0, 0, 1e-14, 1e-14]], np.float32))
+
+
 def test_peaks_large_random_vs_oracle():
     """128x128 maps with plateaus, saturation, every kernel shape; bit-exact."""
     H = W = 128
