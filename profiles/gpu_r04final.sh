@@ -2,7 +2,7 @@
 # CPU baseline; C, D, E; A detect / module), rocprofv3 kernel trace of B, and a
 # 2-rank gloo rehearsal on the one card (physical_gpus = 1).
 set -o pipefail
-O=gpurun_out/r04final
+O=gpurun_out/${1:-r04final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 $O/gpu_tests.log; exit 1; }
