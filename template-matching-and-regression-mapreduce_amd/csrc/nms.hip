@@ -295,6 +295,125 @@ __global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restr
     if (tid == 0) kept_out[g] = cnt;
 }
 
+// Calls whose every image has at most SMALL_N candidates (the module API's
+// one image of a few exemplars, demo.py:123-130): the whole NMS of an image
+// in ONE workgroup -- gather, the stable descending sort as a rank count over
+// rocprim's float key order (so the same order as the radix sort: -0.0 ==
+// +0.0, ties by local index), the IoU words in LDS with mask_strip's
+// arithmetic, and the greedy chain -- one launch instead of gather + sort
+// + strips, no work buffer.  Same keep lists by construction.
+constexpr int SMALL_N = 256;
+
+__device__ __forceinline__ uint32_t radix_key(float f) {
+    uint32_t b = __float_as_uint(f);
+    if (b == 0x80000000u) b = 0u;  // rocprim's digit extractor: -0.0 sorts as +0.0
+    return b ^ ((b & 0x80000000u) ? 0xffffffffu : 0x80000000u);
+}
+
+__global__ __launch_bounds__(SMALL_N) void nms_small_kernel(
+    const float *__restrict__ logits, const float *__restrict__ box, const float *__restrict__ ref,
+    const int32_t *__restrict__ counts, const int64_t *__restrict__ unit_off,
+    const int32_t *__restrict__ seg_units, const int64_t *__restrict__ cand_off, double thr,
+    float *__restrict__ out_logits, float *__restrict__ out_boxes, float *__restrict__ out_refs,
+    int64_t *__restrict__ out_keep, int32_t *__restrict__ kept_out) {
+    __shared__ float ss[SMALL_N];
+    __shared__ float4 ub[SMALL_N];   // unit order
+    __shared__ float2 ur[SMALL_N];
+    __shared__ uint32_t key[SMALL_N];
+    __shared__ int order[SMALL_N];   // sorted position -> local index
+    __shared__ float4 sb[SMALL_N];   // sorted order
+    __shared__ float sa[SMALL_N];
+    __shared__ uint64_t mask[SMALL_N][SMALL_N / 64];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int64_t off = cand_off[g];
+    const int n = min((int)(cand_off[g + 1] - off), SMALL_N);
+    int pos = 0;
+    for (int u = seg_units[g]; u < seg_units[g + 1]; ++u) {  // gather_kernel's union
+        const int c = counts[u];
+        if (c == 0) {
+            if (tid == 0 && pos < n) {
+                ss[pos] = 0.0f;
+                ub[pos] = float4{0.0f, 0.0f, 1e-14f, 1e-14f};
+                ur[pos] = float2{0.0f, 0.0f};
+            }
+            pos += 1;
+            continue;
+        }
+        const size_t src = (size_t)unit_off[u];
+        for (int i = tid; i < c && pos + i < n; i += SMALL_N) {  // (n from the host's counts)
+            ss[pos + i] = logits[2 * (src + i)];
+            ub[pos + i] = reinterpret_cast<const float4 *>(box)[src + i];
+            ur[pos + i] = float2{ref[2 * (src + i) + 0], ref[2 * (src + i) + 1]};
+        }
+        pos += c;
+    }
+    __syncthreads();
+    if (tid < n) key[tid] = radix_key(ss[tid]);
+    __syncthreads();
+    if (tid < n) {
+        const uint32_t k = key[tid];
+        int r = 0;
+        for (int j = 0; j < n; ++j) {
+            const uint32_t kj = key[j];
+            r += (kj > k) | ((kj == k) & (j < tid));
+        }
+        order[r] = tid;
+    }
+    __syncthreads();
+    if (tid < n) {
+        const float4 b = ub[order[tid]];
+        sb[tid] = b;
+        sa[tid] = (b.z - b.x) * (b.w - b.y);
+    }
+    __syncthreads();
+    const int nb = (n + 63) / 64;
+    for (int t = tid; t < n * nb; t += SMALL_N) {  // word q of sorted row i
+        const int i = t / nb, q = t - i * nb;
+        const float4 bi = sb[i];
+        const float ai = sa[i];
+        uint64_t bits = 0;
+        const int jhi = min(64, n - q * 64);
+        for (int k = 0; k < jhi; ++k) {
+            const int j = q * 64 + k;
+            const float4 bj = sb[j];
+            const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+            const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+            float ww = xx2 - xx1, hh = yy2 - yy1;
+            ww = ww > 0.0f ? ww : 0.0f;
+            hh = hh > 0.0f ? hh : 0.0f;
+            const float inter = ww * hh;
+            const float ovr = inter / (ai + sa[j] - inter);
+            if (j > i && (double)ovr > thr) bits |= (1ull << k);
+        }
+        mask[i][q] = bits;
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: lane q < nb holds word q of the removed bitmap
+        uint64_t rem = 0;
+        int cnt = 0;
+        for (int i = 0; i < n; ++i) {
+            const uint64_t mine = tid == (i >> 6) ? rem : 0ull;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, i >> 6);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), i >> 6);
+            const uint64_t w = ((uint64_t)hi << 32) | lo;
+            if ((w >> (i & 63)) & 1ull) continue;  // wave-uniform
+            if (tid == 0) {
+                const int li = order[i];
+                const int64_t dst = off + cnt;
+                out_logits[2 * dst + 0] = ss[li];
+                out_logits[2 * dst + 1] = 0.0f;
+                reinterpret_cast<float4 *>(out_boxes)[dst] = ub[li];
+                out_refs[2 * dst + 0] = ur[li].x;
+                out_refs[2 * dst + 1] = ur[li].y;
+                if (out_keep) out_keep[dst] = li;
+            }
+            ++cnt;
+            if (tid < nb) rem |= mask[i][tid];
+        }
+        if (tid == 0) kept_out[g] = cnt;
+    }
+}
+
 }  // namespace
 
 extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
@@ -318,6 +437,12 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     TMR_REQUIRE(max_nb < (1 << 20) && G < 65536);
     TMR_REQUIRE(max_nb * 8 <= 150 * 1024);  // the removed bitmap in LDS
     hipStream_t s = tmr_stream(stream);
+    if (max_cand <= SMALL_N) {  // every image fits one workgroup
+        hipLaunchKernelGGL(nms_small_kernel, dim3(G), dim3(SMALL_N), 0, s, logits, box, ref, counts, unit_off,
+                           seg_units, cand_off, iou_threshold, out_logits, out_boxes, out_refs, out_keep, kept);
+        TMR_CHECK_LAUNCH();
+        return TMR_OK;
+    }
     int64_t S, strip_words;
     strip_plan(sum_nb, max_nb, S, strip_words);
     NmsWork w = carve(work, total_cand, sum_nb, strip_words, G);

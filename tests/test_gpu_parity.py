@@ -610,6 +610,45 @@ def test_nms_random_vs_oracle(n, thr):
     assert np.array_equal(keep.cpu().numpy(), oracle.nms(bx, sc, thr))
 
 
+def _nms_case(seed, n):
+    u = synth.uniform(seed, 5 * n).reshape(n, 5).astype(np.float32)
+    xy = u[:, :2] * 0.5
+    bx = np.concatenate([xy, xy + 0.01 + u[:, 2:4] * 0.3], 1).astype(np.float32)
+    sc = (np.round(u[:, 4] * 16) / 16).astype(np.float32)  # many ties
+    return bx, sc
+
+
+def test_nms_small_images_one_workgroup_path():
+    """Calls whose images all hold <= 256 candidates run the one-workgroup
+    kernel; a call with a larger image runs gather + radix sort + strips for
+    every image.  The same image gives the same kept rows and order either
+    way -- ties, duplicate boxes, zero-area boxes, -0.0 / +0.0 and NaN
+    scores included -- and equals the oracle where it is defined (no NaN)."""
+    big_bx, big_sc = _nms_case(501, 900)
+    for seed, n in ((502, 1), (503, 17), (504, 64), (505, 65), (506, 200), (507, 256)):
+        bx, sc = _nms_case(seed, n)
+        if n >= 17:
+            bx[3] = bx[5]; sc[3] = sc[5]  # duplicate row
+            bx[7, 2:] = bx[7, :2]  # zero area
+            sc[8], sc[9] = -0.0, 0.0
+        for with_nan in (False, True):
+            s2 = sc.copy()
+            if with_nan and n >= 17:
+                s2[11] = np.nan
+            lg = np.stack([s2, np.zeros_like(s2)], 1)
+            lgb = np.stack([big_sc, np.zeros_like(big_sc)], 1)
+            for thr in (0.15, 0.5):
+                L1, B1, R1 = tmr_amd.NMS([cuda(lg)], [cuda(bx)], [cuda(bx[:, :2].copy())], thr)
+                L2, B2, R2 = tmr_amd.NMS([cuda(lg), cuda(lgb)], [cuda(bx), cuda(big_bx)],
+                                         [cuda(bx[:, :2].copy()), cuda(big_bx[:, :2].copy())], thr)
+                assert bits_equal(L1[0].cpu().numpy(), L2[0].cpu().numpy()), (n, with_nan, thr)
+                assert bits_equal(B1[0].cpu().numpy(), B2[0].cpu().numpy()), (n, with_nan, thr)
+                assert bits_equal(R1[0].cpu().numpy(), R2[0].cpu().numpy()), (n, with_nan, thr)
+                if not with_nan:
+                    keep = oracle.nms(bx, s2, thr)
+                    assert bits_equal(B1[0].cpu().numpy(), bx[keep]), (n, thr)
+
+
 # ----------------------------------------------------------------- callers
 def test_caller_sequence_golden(golden):
     """demo.Inference.infer / each_step_multi_exemplars through TMREngine.detect."""
