@@ -696,9 +696,9 @@ class TMREngine:
             done = torch.cuda.Event()
             done.record(side)
         acc0.record_stream(main)
-        for t in (xmax0, bplane):  # (None under the bf16 contract / without the fold)
-            if t is not None:
-                t.record_stream(side)
+        xmax0.record_stream(side)
+        if bplane is not None:
+            bplane.record_stream(side)
         if self.reuse_image_work:
             self._acc0_store(feats, split, H, W, acc0)
         return acc0, done
