@@ -409,7 +409,6 @@ class TMREngine:
         self._fp_memo = None
         self._acc0_memo = None
         self._graphs: Dict[tuple, _DetectGraph] = {}
-        self._side_streams: Dict[int, "torch.cuda.Stream"] = {}
         self._graph_seen: Dict[tuple, int] = {}
         self.last_graph = None
         self.last_graph_error = None
@@ -669,40 +668,6 @@ class TMREngine:
         self._memo_absmax(out, "ftm", lambda: absmax(slots))
         return out, relu
 
-    # the shared fp half (tmr_split_conv_store) on a side stream, joined
-    # before the heads launch (profiles/r04s)
-    overlap_store = True
-
-    def _store_side(self, feats, split, H, W, N, B, ks, pc, xmax0, bplane, acc16):
-        """Record pack of up2x(feats) + the fp-half store on the device's side
-        stream (forked from the current one); returns (acc0, its done event).
-        acc0 is recorded on the current stream too (the heads read it)."""
-        dev = feats.device
-        main = torch.cuda.current_stream(dev)
-        side = self._side_streams.get(dev.index)
-        if side is None:
-            side = self._side_streams[dev.index] = torch.cuda.Stream(dev)
-        side.wait_stream(main)
-        wp_fp, _, zero_b = split
-        with torch.cuda.stream(side):
-            xp0 = pack_split_up(feats, self.cfg.feature_upsample, ks, self.cfg.precision, xmax0, ones=False)
-            acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev, dtype=torch.float32)
-            fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0)
-            if bplane is not None:
-                fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
-            call("tmr_split_conv_store", ptr(xp0), int(feats.shape[1]), None, None, 0, B, H, W, ks, pc,
-                 ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0,
-                 ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
-            done = torch.cuda.Event()
-            done.record(side)
-        acc0.record_stream(main)
-        xmax0.record_stream(side)
-        if bplane is not None:
-            bplane.record_stream(side)
-        if self.reuse_image_work:
-            self._acc0_store(feats, split, H, W, acc0)
-        return acc0, done
-
     def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
                feats: Optional[torch.Tensor] = None):
         """Decoders + heads over cat([fp[img(u)], f_TM[u]]) -> o [U,1,H,W], b [U,4,H,W]|None.
@@ -741,7 +706,7 @@ class TMREngine:
                 bplane = self._bias_plane(wbias, H, W)
             nparts = load().tmr_heads_partials_size(N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
-            acc0 = store_done = None
+            acc0 = None
             C0k = C0
             pc = prec_code(cfg.precision)
             if fold:
@@ -755,16 +720,8 @@ class TMREngine:
                     # its own activation scale
                     xmax1 = tm_max
                     acc0 = self._acc0_lookup(feats, split, H, W)
-                    if acc0 is None and self.overlap_store:
-                        # the fp half (its record pack + the store launch) on a
-                        # side stream: the f_TM record pack below then runs
-                        # beside the store, whose blocks leave it room
-                        acc0, store_done = self._store_side(feats, split, H, W, N, B, ks, pc, xmax0,
-                                                            bplane, acc16)
-                        xp0 = None
-                    else:
-                        xp0 = None if acc0 is not None else \
-                            pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0, ones=False)
+                    xp0 = None if acc0 is not None else \
+                        pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0, ones=False)
                 else:
                     # ONE launch reads both sources and undoes ONE activation
                     # scale (conv_split.hip takes one xmax per launch): both
@@ -801,10 +758,8 @@ class TMREngine:
                          ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
                     if fold and self.reuse_image_work:
                         self._acc0_store(feats, split, H, W, acc0)
-                # else: the image's cached fp half (or the side stream's store)
+                # else: the image's cached fp half
                 wp, src0, C0k = wp_tm, None, 0
-            if store_done is not None:
-                torch.cuda.current_stream(dev).wait_event(store_done)
             ev = None
             if self.decoder_events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

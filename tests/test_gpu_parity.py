@@ -665,28 +665,6 @@ def test_caller_sequence_golden(golden):
         assert bits_equal(R[0].cpu().numpy(), g[f"{tag}_refs"])
 
 
-def test_store_side_stream_bitexact():
-    """The shared fp half (tmr_split_conv_store) on the side stream, joined
-    before the heads launch, gives the same bits as the same work on one
-    stream -- for several forwards queued back to back."""
-    B, E = 2, 3
-    P = synth.reference_state_dict(4, cin=64, emb=128, obj_bias=-0.5)
-    eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()}, tmr_amd.PathConfig(emb_dim=128))
-    ui = np.repeat(np.arange(B), E)
-    runs = {}
-    for overlap in (False, True):
-        eng.overlap_store = overlap
-        outs = []
-        for seed in range(3):
-            feats = cuda(synth.sam_features(30 + seed, B, 64, 32, 32))
-            ex, _ = synth.exemplar_set(40 + seed, B, E, 64, 64, 3, 11)
-            outs.append(eng.forward_units(feats, ui, ex.reshape(-1, 4)))
-        runs[overlap] = [(r["o"].cpu().numpy(), r["b"].cpu().numpy()) for r in outs]
-    assert eng.last_shared_flops > 0
-    for (o0, b0), (o1, b1) in zip(runs[False], runs[True]):
-        assert bits_equal(o0, o1) and bits_equal(b0, b1)
-
-
 def test_shared_fp_half_matches_unshared():
     """conv(cat[fp,f_TM]) computed as conv_fp (once per image) + conv_tm (per
     unit) agrees with the single fused conv within the fp32 contract."""
