@@ -94,6 +94,23 @@ def test_pmc_fields_tied_to_kernel_sources(tmp_path, monkeypatch):
     assert b.load_pmc("C", "heads") == (None, "no PMC record for this config")
 
 
+def test_committed_pmc_records_match_this_tree():
+    """Every record of the committed profiles/pmc_by_config.json was collected
+    on the kernel sources of this tree (so every bench line's traffic /
+    mfma_busy_pmc is live): a kernel edit without re-running
+    profiles/gpu_pmc.sh turns this red."""
+    import json
+    from tmr_amd import buildinfo
+    d = json.load(open(os.path.join(REPO, "profiles", "pmc_by_config.json")))
+    stale = []
+    for cfg, roles in d["configs"].items():
+        for role, rec in roles.items():
+            if isinstance(rec, dict) and rec.get("source_digest") != buildinfo.source_digest(role):
+                stale.append(f"{cfg}/{role}")
+    assert set(d["configs"]) >= {"A", "B", "C", "D", "E"}
+    assert not stale, f"PMC records from other kernel sources: {stale} (re-run profiles/gpu_pmc.sh)"
+
+
 def test_frac_guard_nulls_fractions_above_one():
     b = _bench()
     out = {"roofline": {"frac": 0.2, "executed_frac": 1.3, "nested": {"x_frac": 2.0, "n": 5}}, "frac": 0.9}
