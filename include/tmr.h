@@ -305,6 +305,19 @@ int tmr_nms(const float *logits, const float *box, const float *ref, const int32
             int G, int64_t total_cand, int64_t max_cand, int64_t sum_nb, double iou_threshold,
             float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
             int32_t *kept, void *work, void *stream);
+/* tmr_nms for images of at most TMR_NMS_SMALL candidates, sized on the
+ * DEVICE from counts (no host sync before it, so it can follow the peak
+ * finder inside one captured forward): image g's kept rows are written at
+ * row g * TMR_NMS_SMALL of out_logits [G*TMR_NMS_SMALL,2] / out_boxes [.,4] /
+ * out_refs [.,2] (+ out_keep, nullable), kept[g] = their count -- the same
+ * rows and order tmr_nms produces -- or kept[g] = -1 when the image's union
+ * exceeds TMR_NMS_SMALL rows (then nothing is written for it: run tmr_nms).
+ * One workgroup per image, no work memory. */
+#define TMR_NMS_SMALL 256
+int tmr_nms_small(const float *logits, const float *box, const float *ref, const int32_t *counts,
+                  const int64_t *unit_off, const int32_t *seg_units, int G, double iou_threshold,
+                  float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
+                  int32_t *kept, void *stream);
 
 /* ---- (§8f f1) streaming mapper statistics ---------------------------------
  * Per image b of x [B][n] fp32 (the backbone feature the mapper computes,

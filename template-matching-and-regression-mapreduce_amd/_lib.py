@@ -87,6 +87,7 @@ SIGNATURES = {
     "tmr_maxpool3x3": (_I, [_P, _L, _I, _I, _I, _P, _P]),
     "tmr_nms_work_size": (_L, [_L, _L, _L, _I]),
     "tmr_nms": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _L, _L, _L, _D, _P, _P, _P, _P, _P, _P, _P]),
+    "tmr_nms_small": (_I, [_P, _P, _P, _P, _P, _P, _I, _D, _P, _P, _P, _P, _P, _P]),
     "tmr_feature_stats_work_size": (_L, [_I]),
     "tmr_feature_stats": (_I, [_P, _I, _L, _P, _P, _P]),
     "tmr_exp_table_encode": (_L, [_P, _L, _P, _L]),

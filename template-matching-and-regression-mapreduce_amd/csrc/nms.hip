@@ -302,7 +302,7 @@ __global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restr
 // +0.0, ties by local index), the IoU words in LDS with mask_strip's
 // arithmetic, and the greedy chain -- one launch instead of gather + sort
 // + strips, no work buffer.  Same keep lists by construction.
-constexpr int SMALL_N = 256;
+constexpr int SMALL_N = TMR_NMS_SMALL;
 
 __device__ __forceinline__ uint32_t radix_key(float f) {
     uint32_t b = __float_as_uint(f);
@@ -310,12 +310,13 @@ __device__ __forceinline__ uint32_t radix_key(float f) {
     return b ^ ((b & 0x80000000u) ? 0xffffffffu : 0x80000000u);
 }
 
-__global__ __launch_bounds__(SMALL_N) void nms_small_kernel(
+// one image's union (units u_beg..u_end-1, n <= SMALL_N rows) -> kept rows at
+// out[off ...], kept_out[g]; one workgroup of SMALL_N threads
+__device__ __forceinline__ void nms_small_image(
     const float *__restrict__ logits, const float *__restrict__ box, const float *__restrict__ ref,
-    const int32_t *__restrict__ counts, const int64_t *__restrict__ unit_off,
-    const int32_t *__restrict__ seg_units, const int64_t *__restrict__ cand_off, double thr,
-    float *__restrict__ out_logits, float *__restrict__ out_boxes, float *__restrict__ out_refs,
-    int64_t *__restrict__ out_keep, int32_t *__restrict__ kept_out) {
+    const int32_t *__restrict__ counts, const int64_t *__restrict__ unit_off, int u_beg, int u_end, int n,
+    int64_t off, double thr, float *__restrict__ out_logits, float *__restrict__ out_boxes,
+    float *__restrict__ out_refs, int64_t *__restrict__ out_keep, int32_t *__restrict__ kept_out, int g) {
     __shared__ float ss[SMALL_N];
     __shared__ float4 ub[SMALL_N];   // unit order
     __shared__ float2 ur[SMALL_N];
@@ -324,11 +325,9 @@ __global__ __launch_bounds__(SMALL_N) void nms_small_kernel(
     __shared__ float4 sb[SMALL_N];   // sorted order
     __shared__ float sa[SMALL_N];
     __shared__ uint64_t mask[SMALL_N][SMALL_N / 64];
-    const int g = blockIdx.x, tid = threadIdx.x;
-    const int64_t off = cand_off[g];
-    const int n = min((int)(cand_off[g + 1] - off), SMALL_N);
+    const int tid = threadIdx.x;
     int pos = 0;
-    for (int u = seg_units[g]; u < seg_units[g + 1]; ++u) {  // gather_kernel's union
+    for (int u = u_beg; u < u_end; ++u) {  // gather_kernel's union
         const int c = counts[u];
         if (c == 0) {
             if (tid == 0 && pos < n) {
@@ -414,6 +413,40 @@ __global__ __launch_bounds__(SMALL_N) void nms_small_kernel(
     }
 }
 
+__global__ __launch_bounds__(SMALL_N) void nms_small_kernel(
+    const float *__restrict__ logits, const float *__restrict__ box, const float *__restrict__ ref,
+    const int32_t *__restrict__ counts, const int64_t *__restrict__ unit_off,
+    const int32_t *__restrict__ seg_units, const int64_t *__restrict__ cand_off, double thr,
+    float *__restrict__ out_logits, float *__restrict__ out_boxes, float *__restrict__ out_refs,
+    int64_t *__restrict__ out_keep, int32_t *__restrict__ kept_out) {
+    const int g = blockIdx.x;
+    const int64_t off = cand_off[g];
+    const int n = min((int)(cand_off[g + 1] - off), SMALL_N);
+    nms_small_image(logits, box, ref, counts, unit_off, seg_units[g], seg_units[g + 1], n, off, thr,
+                    out_logits, out_boxes, out_refs, out_keep, kept_out, g);
+}
+
+// The same with the union sizes taken from the DEVICE counts (no host sync
+// first): image g's rows go to g * SMALL_N; an image whose union exceeds
+// SMALL_N rows gets kept[g] = -1 and is left to tmr_nms.
+__global__ __launch_bounds__(SMALL_N) void nms_small_dev_kernel(
+    const float *__restrict__ logits, const float *__restrict__ box, const float *__restrict__ ref,
+    const int32_t *__restrict__ counts, const int64_t *__restrict__ unit_off,
+    const int32_t *__restrict__ seg_units, double thr, float *__restrict__ out_logits,
+    float *__restrict__ out_boxes, float *__restrict__ out_refs, int64_t *__restrict__ out_keep,
+    int32_t *__restrict__ kept_out) {
+    const int g = blockIdx.x;
+    const int u_beg = seg_units[g], u_end = seg_units[g + 1];
+    int64_t n = 0;
+    for (int u = u_beg; u < u_end; ++u) n += max(counts[u], 1);  // (block-uniform)
+    if (n > SMALL_N) {
+        if (threadIdx.x == 0) kept_out[g] = -1;
+        return;
+    }
+    nms_small_image(logits, box, ref, counts, unit_off, u_beg, u_end, (int)n, (int64_t)g * SMALL_N, thr,
+                    out_logits, out_boxes, out_refs, out_keep, kept_out, g);
+}
+
 }  // namespace
 
 extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
@@ -421,6 +454,19 @@ extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t
     int64_t S, words;
     strip_plan(sum_nb, (max_cand + 63) / 64, S, words);
     return work_bytes(total_cand, sum_nb, words, G);
+}
+
+extern "C" int tmr_nms_small(const float *logits, const float *box, const float *ref, const int32_t *counts,
+                             const int64_t *unit_off, const int32_t *seg_units, int G, double iou_threshold,
+                             float *out_logits, float *out_boxes, float *out_refs, int64_t *out_keep,
+                             int32_t *kept, void *stream) {
+    TMR_REQUIRE(logits && box && ref && counts && unit_off && seg_units && out_logits && out_boxes && out_refs);
+    TMR_REQUIRE(kept && G > 0 && G < 65536);
+    hipLaunchKernelGGL(nms_small_dev_kernel, dim3(G), dim3(SMALL_N), 0, tmr_stream(stream), logits, box, ref,
+                       counts, unit_off, seg_units, iou_threshold, out_logits, out_boxes, out_refs, out_keep,
+                       kept);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
 }
 
 extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,

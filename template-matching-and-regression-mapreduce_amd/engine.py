@@ -37,6 +37,7 @@ from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16
 
 NHEAD = 5
 ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
+NMS_SMALL = 256  # TMR_NMS_SMALL (include/tmr.h)
 
 
 @dataclass
@@ -399,6 +400,7 @@ class TMREngine:
         # "valu" or "mfma" (csrc/xcorr.hip)
         self.xcorr_algo = "auto"
         self.last_xcorr_algo = None
+        self.last_nms_small = False  # detect: the kept rows came from the in-forward small NMS
         # bf16 contract, detect path: the one-term MFMA correlation writes
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
@@ -1065,18 +1067,38 @@ class TMREngine:
                 tuple((k, t.data_ptr(), t._version) for k, t in sorted(self.P.items())))
 
     @staticmethod
-    def _detect_host_inputs(units, unit_image, B, params) -> Dict[str, np.ndarray]:
-        """The tagged host inputs of detect's forward, as _h2d stages them."""
-        return {"units": units.view(np.uint8), "img_units": np.asarray(host.image_ranges(unit_image, B)),
-                "unit_image": np.asarray(unit_image, np.int32), "unit_image64": np.asarray(unit_image, np.int64),
-                "peak_params": params.view(np.uint8)}
+    def _detect_host_inputs(units, unit_image, B, params, nms_in=None) -> Dict[str, np.ndarray]:
+        """The tagged host inputs of detect's forward, as _h2d stages them
+        (nms_in: the speculative small NMS's (unit_off, seg) arrays)."""
+        d = {"units": units.view(np.uint8), "img_units": np.asarray(host.image_ranges(unit_image, B)),
+             "unit_image": np.asarray(unit_image, np.int32), "unit_image64": np.asarray(unit_image, np.int64),
+             "peak_params": params.view(np.uint8)}
+        if nms_in is not None:
+            d["nms_unit_off"], d["nms_seg"] = nms_in
+        return d
 
-    def _forward_peaks(self, feats, unit_image, boxes, params):
+    def _forward_peaks(self, feats, unit_image, boxes, params, nms=None):
+        """forward + peak finder; with nms = (unit_off, seg, iou_threshold)
+        also the device-sized small NMS (tmr_nms_small) and one int32 tensor
+        [counts..., kept...] to read back with a single sync."""
         r = self.forward_units(feats, unit_image, boxes)
         logits, box, ref, counts, _ = self.peaks(r["o"], r["b"], params)
-        return logits, box, ref, counts
+        if nms is None:
+            return logits, box, ref, counts
+        unit_off, seg, iou = nms
+        dev = logits.device
+        G = len(seg) - 1
+        uo = _h2d(unit_off, dev, tag="nms_unit_off")
+        sg = _h2d(seg, dev, tag="nms_seg")
+        out_l = torch.empty((G * NMS_SMALL, 2), device=dev, dtype=torch.float32)
+        out_b = torch.empty((G * NMS_SMALL, 4), device=dev, dtype=torch.float32)
+        out_r = torch.empty((G * NMS_SMALL, 2), device=dev, dtype=torch.float32)
+        kept = torch.empty(G, device=dev, dtype=torch.int32)
+        call("tmr_nms_small", ptr(logits), ptr(box), ptr(ref), ptr(counts), ptr(uo), ptr(sg), G, float(iou),
+             ptr(out_l), ptr(out_b), ptr(out_r), None, ptr(kept), stream())
+        return logits, box, ref, counts, torch.cat([counts, kept]), out_l, out_b, out_r
 
-    def _capture_detect(self, feats, unit_image, boxes, params, host_in):
+    def _capture_detect(self, feats, unit_image, boxes, params, host_in, nms=None):
         """Capture _forward_peaks on a static copy of feats (caches built by
         the eager call that preceded).  None if capture fails (eager then)."""
         static = feats.detach().float().contiguous().clone()
@@ -1086,7 +1108,7 @@ class TMREngine:
         _capture.slots, _capture.used = slots, set()
         try:
             with torch.cuda.graph(graph):
-                out = self._forward_peaks(static, unit_image, boxes, params)
+                out = self._forward_peaks(static, unit_image, boxes, params, nms)
             used = _capture.used
         except Exception as err:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
             self.last_graph_error = f"{type(err).__name__}: {err}"
@@ -1116,32 +1138,52 @@ class TMREngine:
         H, W = (2 * Hin, 2 * Win) if self.cfg.feature_upsample else (Hin, Win)
         params = host.peak_params(boxes, H, W, cls_ths, self.cfg.box_reg, ablation_b, ablation_c)
         C = int(self.P["input_proj.0.weight"].shape[0])
-        sig = units = None
+        U = B * E
+        unit_off = np.arange(U, dtype=np.int64) * (H * W)
+        seg = np.arange(0, U + 1, E, dtype=np.int64)
+        sig = units = nms_in = None
         if self.use_graphs and len(unit_image) <= self.GRAPH_MAX_UNITS:  # else no graph prep at all
             units = host.build_units(boxes, unit_image, H, W, C, self.cfg.template_type)[0] \
                 if not self.cfg.no_matcher else np.zeros(0, UNIT_DTYPE)
             sig = self._graph_signature(feats, units, unit_image, ablation_b, ablation_c)
+            # small batches also run the device-sized small NMS in the same
+            # forward (tmr_nms_small): one sync instead of two when every
+            # image's union fits NMS_SMALL rows (else tmr_nms after the sync)
+            nms_in = (unit_off, seg.astype(np.int32))
+            if sig is not None:
+                sig = sig + (float(iou_threshold),)  # a kernel argument of the captured NMS
+        spec = (unit_off, seg.astype(np.int32), iou_threshold) if nms_in is not None else None
         g = self._graphs.get(sig) if sig is not None else None
         self.last_graph = "replay" if g is not None else "eager"
         if g is None and sig is not None:
             self._graph_seen[sig] = self._graph_seen.get(sig, 0) + 1
             if self._graph_seen[sig] >= 2:
                 g = self._capture_detect(feats, unit_image, boxes, params, self._detect_host_inputs(
-                    units, unit_image, B, params))
+                    units, unit_image, B, params, nms_in), spec)
                 if g is not None:
                     if len(self._graphs) >= self.GRAPH_CACHE:
                         self._graphs.pop(next(iter(self._graphs)))
                     self._graphs[sig] = g
                     self.last_graph = "captured"
         if g is not None:
-            host_in = self._detect_host_inputs(units, unit_image, B, params)
-            logits, box, ref, counts = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
+            host_in = self._detect_host_inputs(units, unit_image, B, params, nms_in)
+            out = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
             for k, v in g.last.items():
                 setattr(self, k, v)
         else:
-            logits, box, ref, counts = self._forward_peaks(feats, unit_image, boxes, params)
-        counts_host = counts.cpu().numpy()  # torch.where-style sync (TM_utils.py:254)
-        U = B * E
-        unit_off = np.arange(U, dtype=np.int64) * (H * W)  # staged by nms with its other host arrays
-        seg = np.arange(0, U + 1, E, dtype=np.int64)
+            out = self._forward_peaks(feats, unit_image, boxes, params, spec)
+        logits, box, ref, counts = out[:4]
+        if spec is not None:
+            ck = out[4].cpu().numpy()  # torch.where-style sync (TM_utils.py:254): counts + kept
+            counts_host, kept = ck[:U], ck[U:]
+            self.last_nms_small = bool((kept >= 0).all())
+            if self.last_nms_small:
+                # graph outputs are the graph's static buffers: copied out
+                ol, ob, orf = (t.clone() for t in out[5:8]) if g is not None else out[5:8]
+                s0 = [int(i) * NMS_SMALL for i in range(B)]
+                return ([ol[a:a + int(k)] for a, k in zip(s0, kept)], [ob[a:a + int(k)] for a, k in zip(s0, kept)],
+                        [orf[a:a + int(k)] for a, k in zip(s0, kept)])
+        else:
+            counts_host = counts.cpu().numpy()  # torch.where-style sync (TM_utils.py:254)
+            self.last_nms_small = False
         return self.nms(logits, box, ref, counts, counts_host, unit_off, seg, iou_threshold)

@@ -999,6 +999,19 @@ def test_detect_graph_replay_matches_eager():
                 assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (seed, eng.last_graph)
     assert modes[0] == "eager" and modes[1] == "captured" and modes[2:] == ["replay"] * 3, \
         (modes, eng.last_graph_error)
+    # the in-forward small NMS (tmr_nms_small, one sync) and its fallback to
+    # tmr_nms when an image's union exceeds TMR_NMS_SMALL rows: both equal
+    # the eager engine's separate NMS, through eager, capture and replay
+    small = []
+    for cls in (0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5):
+        feats = cuda(synth.sam_features(46, B, cin, hf, hf))
+        got = eng.detect(feats, ex0, cls, 0.3)
+        small.append(eng.last_nms_small)
+        want = ref.detect(feats, ex0, cls, 0.3)
+        for g_, w_ in zip(got, want):
+            for a, b in zip(g_, w_):
+                assert bits_equal(a.cpu().numpy(), b.cpu().numpy()), (cls, eng.last_graph)
+    assert small[:3] == [True] * 3 and small[3:6] == [False] * 3, small
     # a weight update is a new signature: eager again, never a stale replay
     with torch.no_grad():
         eng.P["objectness_head.head.0.bias"].add_(0.1)
