@@ -1003,8 +1003,8 @@ def test_detect_graph_replay_matches_eager():
     # tmr_nms when an image's union exceeds TMR_NMS_SMALL rows: both equal
     # the eager engine's separate NMS, through eager, capture and replay
     small = []
-    for cls in (0.9, 0.9, 0.9, 0.02, 0.02, 0.02, 0.5):
-        feats = cuda(synth.sam_features(46, B, cin, hf, hf))
+    for cls, h2 in ((0.9, hf), (0.9, hf), (0.9, hf), (0.0, 2 * hf), (0.0, 2 * hf), (0.0, 2 * hf), (0.5, hf)):
+        feats = cuda(synth.sam_features(46, B, cin, h2, h2))
         got = eng.detect(feats, ex0, cls, 0.3)
         small.append(eng.last_nms_small)
         want = ref.detect(feats, ex0, cls, 0.3)
