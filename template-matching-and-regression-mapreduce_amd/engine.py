@@ -305,9 +305,45 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
 
 
 # graph capture of TMREngine.detect's forward (_DetectGraph): while set, every
-# host input staged by _h2d is kept under its tag, so that a replay can refill
-# the same pinned buffer the captured copy node reads
+# tagged host input staged by _h2d is a view of the capture's _HostBlob
 _capture = threading.local()
+
+
+class _HostBlob:
+    """The tagged host inputs of a captured forward in ONE pinned buffer and
+    ONE device buffer: the capture's first node copies the pinned bytes up,
+    every tagged _h2d inside the capture is a view of the device buffer, and a
+    replay only rewrites the pinned bytes -- one copy node per forward instead
+    of one per input (each is a ~5 us blit on the GPU's timeline)."""
+
+    def __init__(self, host_in: Dict[str, np.ndarray], device):
+        self.offs: Dict[str, tuple] = {}
+        o = 0
+        for t, a in host_in.items():
+            if a.nbytes:
+                self.offs[t] = (o, a.nbytes)
+                o += (a.nbytes + 15) // 16 * 16  # 16-B aligned sections
+        self.pinned = torch.empty(max(o, 16), dtype=torch.uint8).pin_memory()
+        self.dev = torch.empty(max(o, 16), dtype=torch.uint8, device=device)
+        self.fill(host_in)
+
+    def fill(self, host: Dict[str, np.ndarray]):
+        pn = self.pinned.numpy()
+        for t, a in host.items():
+            if t in self.offs:
+                o, n = self.offs[t]
+                pn[o:o + n] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+
+    def upload(self):  # inside the capture, before anything reads the inputs
+        self.dev.copy_(self.pinned, non_blocking=True)
+
+    def view(self, tag: Optional[str], t: torch.Tensor) -> torch.Tensor:
+        o, n = self.offs.get(tag, (0, -1)) if tag is not None else (0, -1)
+        if n != t.numel() * t.element_size():
+            raise TMRError(f"host input {tag!r} inside a graph capture has no pre-allocated slot")
+        pn = self.pinned.numpy()
+        pn[o:o + n] = t.numpy().reshape(-1).view(np.uint8)  # (the capture's own values)
+        return self.dev[o:o + n].view(t.dtype).reshape(t.shape)
 
 
 def _h2d(arr: np.ndarray, device, dtype=None, tag: Optional[str] = None) -> torch.Tensor:
@@ -316,49 +352,65 @@ def _h2d(arr: np.ndarray, device, dtype=None, tag: Optional[str] = None) -> torc
     allocator keeps the pinned block until the copy's stream event has
     completed).  A pageable `.to(device)` synchronises the stream, leaving the
     GPU idle while the host prepares the next launches.  Inside a graph
-    capture the pinned buffer is kept under `tag` (the replay rewrites it)."""
+    capture a tagged input is a view of the capture's _HostBlob (the replay
+    rewrites its pinned bytes)."""
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if dtype is not None:
         t = t.to(dtype)
     device = torch.device(device)
     if device.type != "cuda":
         return t.to(device)
-    slots = getattr(_capture, "slots", None)
-    if slots is None:
+    blob = getattr(_capture, "blob", None)
+    if blob is None:
         return t.pin_memory().to(device, non_blocking=True)
-    # capture: the pinned buffer was allocated before the capture began (no
-    # host allocation inside it) and is refilled before every replay
-    pinned = slots.get(tag) if tag is not None else None
-    if pinned is None or pinned.numel() * pinned.element_size() != t.numel() * t.element_size():
-        raise TMRError(f"host input {tag!r} inside a graph capture has no pre-allocated slot")
-    np.copyto(pinned.numpy(), t.numpy().reshape(-1).view(pinned.numpy().dtype))
-    _capture.used.add(tag)
-    return pinned.view(t.dtype).reshape(t.shape).to(device, non_blocking=True)
+    return blob.view(tag, t)
 
 
 def _units_to_device(units: np.ndarray, device, tag: Optional[str] = None) -> torch.Tensor:
     return _h2d(units.view(np.uint8), device, tag=tag)
 
 
+def _clone_outputs(out: Dict[str, object], keep=("fp",)) -> Dict[str, object]:
+    """Fresh copies of a replayed graph's static outputs (a caller may keep
+    one call's maps while the next replay runs): tensors that are contiguous
+    views of one storage (o and b) are copied out by ONE copy of the range
+    they cover; names in `keep` are returned as they are."""
+    res, groups = {}, {}
+    for k, v in out.items():
+        if isinstance(v, torch.Tensor) and k not in keep:
+            groups.setdefault(v.untyped_storage().data_ptr(), []).append(k)
+        else:
+            res[k] = v
+    for ks in groups.values():
+        ts = [out[k] for k in ks]
+        if len(ks) == 1 or not all(t.is_contiguous() for t in ts):
+            res.update({k: out[k].clone() for k in ks})
+            continue
+        lo = min(t.storage_offset() for t in ts)
+        hi = max(t.storage_offset() + t.numel() for t in ts)
+        base = ts[0].as_strided((hi - lo,), (1,), lo).clone()
+        for k, t in zip(ks, ts):
+            res[k] = base.as_strided(t.shape, t.stride(), t.storage_offset() - lo)
+    return res
+
+
 class _DetectGraph:
     """One captured detect forward (projection ... peaks) for a fixed launch
     signature: the inputs are a static feature buffer and the pinned host
-    slots of its tagged host inputs; the outputs the peak finder's static
+    blob of its tagged host inputs; the outputs the forward's static
     buffers.  A replay refills both and launches the whole forward at once."""
 
-    def __init__(self, graph, feats, slots, outputs, last):
-        self.graph, self.feats, self.slots, self.outputs, self.last = graph, feats, slots, outputs, last
-        self.done = None  # event after the last replay: its copy nodes read the pinned slots
+    def __init__(self, graph, feats, blob, outputs, last):
+        self.graph, self.feats, self.blob, self.outputs, self.last = graph, feats, blob, outputs, last
+        self.done = None  # event after the last replay: its copy node reads the pinned blob
         self.src = None  # (tensor ref, version, data_ptr) of the features last copied into feats
 
     def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray]):
-        # the slots are rewritten by the host at once: a previous replay still
-        # queued (two calls with no sync between them) must have read them first
+        # the blob is rewritten by the host at once: a previous replay still
+        # queued (two calls with no sync between them) must have read it first
         if self.done is not None:
             self.done.synchronize()
-        for tag, arr in host.items():
-            dst = self.slots[tag].numpy()
-            np.copyto(dst, np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
+        self.blob.fill(host)
         src = self.src
         if src is None or src[0]() is not feats or src[1] != (feats._version, feats.data_ptr()):
             self.feats.copy_(feats)  # (the module API's later exemplars reuse the image's copy)
@@ -782,8 +834,11 @@ class TMREngine:
             self.last_decoder_flops = 2.0 * H * W * N * (C0k + C1) * ks ** 2 * U
             self.last_shared_flops = 2.0 * H * W * N * C0 * ks ** 2 * B if share else 0.0
             self.last_decoder_algo = "split"
-            o = torch.empty((U, 1, H, W), device=dev, dtype=torch.float32)
-            b = torch.empty((U, 4, H, W), device=dev, dtype=torch.float32) if cfg.box_reg else None
+            # o and b as contiguous views of ONE buffer (a graph replay then
+            # copies both out with one copy, _clone_outputs)
+            ob = torch.empty(U * (5 if cfg.box_reg else 1) * H * W, device=dev, dtype=torch.float32)
+            o = ob[:U * H * W].view(U, 1, H, W)
+            b = ob[U * H * W:].view(U, 4, H, W) if cfg.box_reg else None
             call("tmr_heads_reduce", ptr(part), N, 128, U, H, W, ptr(hb), ptr(o),
                  ptr(b) if b is not None else None, stream())
             return o, b
@@ -872,16 +927,16 @@ class TMREngine:
             self._graphs[sig] = g
             self.last_graph = "captured"
         host_in = self._detect_host_inputs(units, unit_image, B, np.zeros(0, np.uint8))
-        out = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
+        out = g.replay(feats.float().contiguous(), host_in)
         for k, v in g.last.items():
             setattr(self, k, v)
         if hit is None:  # this image's memo: the first-call graph's fp / acc0
             self._rebind_memos(feats, g.fp, g.acc0)
-        return {k: (v.clone() if isinstance(v, torch.Tensor) and k != "fp" else v) for k, v in out.items()}
+        return _clone_outputs(out)
 
     def _capture_module(self, feats, unit_image, boxes, want_aux, hit, host_in):
         static = feats.detach().float().contiguous().clone()
-        slots = {t: torch.empty(a.nbytes, dtype=torch.uint8).pin_memory() for t, a in host_in.items() if a.nbytes}
+        blob = _HostBlob(host_in, feats.device)
         saved = (self._fp_memo, self._acc0_memo)
         if hit is not None:
             self._rebind_memos(static, hit[0], hit[1])  # the capture reads the memo buffers
@@ -889,20 +944,20 @@ class TMREngine:
             self._fp_memo = self._acc0_memo = None
         torch.cuda.synchronize(feats.device)
         graph = torch.cuda.CUDAGraph()
-        _capture.slots, _capture.used = slots, set()
+        _capture.blob = blob
         try:
             with torch.cuda.graph(graph):
+                blob.upload()
                 out = self._forward_units_eager(static, unit_image, boxes, want_aux)
-            used = _capture.used
             fp_acc0 = (self._fp_memo[4], self._acc0_memo[3:6]) if hit is None else (None, None)
         except Exception as err:  # noqa: BLE001 -- stay eager
             self.last_graph_error = f"{type(err).__name__}: {err}"
             self._fp_memo, self._acc0_memo = saved
             return None
         finally:
-            _capture.slots = _capture.used = None
+            _capture.blob = None
         self._fp_memo, self._acc0_memo = saved
-        g = _DetectGraph(graph, static, {t: v for t, v in slots.items() if t in used}, out,
+        g = _DetectGraph(graph, static, blob, out,
                          {k: v for k, v in vars(self).items() if k.startswith("last_") and
                           not k.startswith("last_graph")})
         g.fp, g.acc0 = fp_acc0
@@ -913,7 +968,7 @@ class TMREngine:
         """One matching_net forward per unit (image unit_image[u], exemplar
         unit_boxes[u]).  Returns dict(o, b, f_tm_relu, f0, fp)."""
         unit_image = [int(i) for i in unit_image]
-        if self.reuse_image_work and getattr(_capture, "slots", None) is None:
+        if self.reuse_image_work and getattr(_capture, "blob", None) is None:
             r = self._forward_units_graphed(feats, unit_image, unit_boxes, want_aux)
             if r is not None:
                 return r
@@ -1102,22 +1157,21 @@ class TMREngine:
         """Capture _forward_peaks on a static copy of feats (caches built by
         the eager call that preceded).  None if capture fails (eager then)."""
         static = feats.detach().float().contiguous().clone()
-        slots = {t: torch.empty(a.nbytes, dtype=torch.uint8).pin_memory() for t, a in host_in.items()}
+        blob = _HostBlob(host_in, feats.device)
         torch.cuda.synchronize(feats.device)
         graph = torch.cuda.CUDAGraph()
-        _capture.slots, _capture.used = slots, set()
+        _capture.blob = blob
         try:
             with torch.cuda.graph(graph):
+                blob.upload()
                 out = self._forward_peaks(static, unit_image, boxes, params, nms)
-            used = _capture.used
         except Exception as err:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
             self.last_graph_error = f"{type(err).__name__}: {err}"
             return None
         finally:
-            _capture.slots = _capture.used = None
-        slots = {t: v for t, v in slots.items() if t in used}
+            _capture.blob = None
         last = {k: v for k, v in vars(self).items() if k.startswith("last_") and not k.startswith("last_graph")}
-        return _DetectGraph(graph, static, slots, out, last)
+        return _DetectGraph(graph, static, blob, out, last)
 
     def detect(self, feats: torch.Tensor, exemplars, cls_ths: float, iou_threshold: float,
                ablation_b: bool = False, ablation_c: bool = False):
@@ -1167,7 +1221,7 @@ class TMREngine:
                     self.last_graph = "captured"
         if g is not None:
             host_in = self._detect_host_inputs(units, unit_image, B, params, nms_in)
-            out = g.replay(feats.float().contiguous(), {t: host_in[t] for t in g.slots})
+            out = g.replay(feats.float().contiguous(), host_in)
             for k, v in g.last.items():
                 setattr(self, k, v)
         else:

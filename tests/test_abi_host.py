@@ -355,3 +355,25 @@ def test_image_ranges_small_and_vector_forms_agree():
         for pad in (0, host.SMALL_UNITS):
             with pytest.raises(ValueError):
                 host.image_ranges([0] * pad + bad if bad[0] >= 0 else bad + [0] * pad, 3)
+
+
+def test_clone_outputs_groups_views_of_one_buffer():
+    """engine._clone_outputs (a replayed graph's static outputs copied out):
+    contiguous views of one storage (o, b) come back as views of ONE fresh
+    copy with the same values; other tensors are cloned; `fp` is kept."""
+    import torch
+    from tmr_amd.engine import _clone_outputs
+    ob = torch.arange(50.0)
+    o, b = ob[:10].view(2, 1, 5), ob[10:].view(2, 4, 5)
+    f = torch.arange(7.0)
+    r = _clone_outputs({"o": o, "b": b, "f0": f, "fp": f, "n": 3})
+    assert torch.equal(r["o"], o) and torch.equal(r["b"], b) and torch.equal(r["f0"], f)
+    assert r["fp"] is f and r["n"] == 3
+    assert r["o"].untyped_storage().data_ptr() == r["b"].untyped_storage().data_ptr()
+    assert r["o"].untyped_storage().data_ptr() != ob.untyped_storage().data_ptr()
+    assert r["f0"].untyped_storage().data_ptr() != f.untyped_storage().data_ptr()
+    ob.zero_()
+    assert float(r["b"].sum()) == float(sum(range(10, 50)))
+    nc = torch.arange(12.0).view(3, 4)[:, :2]  # non-contiguous views are cloned one by one
+    r = _clone_outputs({"a": nc, "b": nc.t()})
+    assert torch.equal(r["a"], nc) and torch.equal(r["b"], nc.t())
