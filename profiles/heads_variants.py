@@ -12,6 +12,8 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
   noacc0   no initial-value (acc0) read: accumulators start at zero
   noepi    no heads epilogue: one dummy store per block
   nodma    no LDS-DMA at all (halo and weights never loaded)
+  xl2band  the correlation's band staging reads 4 L2-resident rows instead of the band
+  xl2a     the correlation's A fragments all come from template row 0 (L1/L2-resident)
   wsparseN / tsparseN   decoder weights' / correlation templates' hi part at
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   l2dma    every DMA re-reads the first chunk's halo / first step's weights:
@@ -72,6 +74,12 @@ def variant_source(name: str, src: str) -> str:
                     "    (void)r; (void)dst; (void)voff; (void)soff;")
     if name.startswith("wsparse"):  # weights' hi part to N significant bits (wsparse8, wsparse11)
         return re.sub(r"constexpr int WH_BITS = \d+;", f"constexpr int WH_BITS = {int(name[7:])};", src, count=1)
+    if name == "xl2band":  # correlation band staging reads 4 L2-resident rows (timing only)
+        return _sub(src, "if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];",
+                    "if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(a.f + (size_t)(yy & 3) * W)[cc];")
+    if name == "xl2a":  # correlation A fragments all read from template row 0 (L1/L2-resident; timing only)
+        return _sub(src, "return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);",
+                    "return *reinterpret_cast<const V *>(arow + (size_t)((0 * i + nk) * 2 + term) * AFRAG);")
     if name.startswith("tsparse"):  # correlation templates' hi part (xcorr.hip TH_BITS)
         return _sub(src, "constexpr int TH_BITS = 11;", f"constexpr int TH_BITS = {int(name[7:])};")
     if name == "l2dma":
@@ -86,7 +94,7 @@ def variant_source(name: str, src: str) -> str:
 
 
 def variant_file(name: str) -> str:
-    return "xcorr.hip" if name.startswith("tsparse") else "conv_split.hip"
+    return "xcorr.hip" if name.startswith(("tsparse", "xl2band", "xl2a")) else "conv_split.hip"
 
 
 VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma", "l2dma"]
