@@ -14,8 +14,11 @@ the oracle exactly as the headline tests check the graded batches:
   (oracle/agreement.py).
 
 The configurations are drawn from a fixed seed, so the sweep is the same on
-every run; the 64 take a few seconds of CPU oracle.
+every run; the 64 take a few seconds of CPU oracle.  TMR_RANDOM_SWEEP=N
+widens both sweeps to N seeds (a one-off deep run, e.g. profiles/r04_random*.log).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -28,6 +31,8 @@ from tmr_amd import synth
 pytestmark = pytest.mark.gpu
 
 TOL = {"fp32": 1e-5, "f16": 1e-3, "bf16": 1e-2}
+N_CONFIG = int(os.environ.get("TMR_RANDOM_SWEEP", "64"))
+N_VARIANT = int(os.environ.get("TMR_RANDOM_SWEEP", "32"))
 DEV = torch.device("cuda:0")
 
 
@@ -62,7 +67,7 @@ def draw(seed):
                 precision=str(r.choice(["fp32", "fp32", "fp32", "bf16", "f16"])) if seed >= 24 else "fp32")
 
 
-@pytest.mark.parametrize("seed", range(64))
+@pytest.mark.parametrize("seed", range(N_CONFIG))
 def test_random_config_vs_oracle(seed):
     c = draw(seed)
     P = synth.reference_state_dict(300 + seed, cin=c["cin"], emb=c["emb"], obj_bias=c["bias"])
@@ -134,7 +139,7 @@ def draw_variant(seed):
         bias=float(r.uniform(-0.5, 0.5)), scale=float(r.uniform(0.5, 1.5)))
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(N_VARIANT))
 def test_random_module_variant_vs_oracle(seed):
     """matching_net built from the reference's args (every architecture
     switch drawn at random) called in the reference's module form, against
