@@ -8,9 +8,9 @@
 //   F16X3  fp32-grade: x = s_x^-1 (xh + xl), w = s_w^-1 (wh + wl) with fp16
 //          hi/lo parts and power-of-two scales s (max |x s| < 2^14), and
 //          x.w ~= (wh xh + wl xh + wh xl) / (s_x s_w), fp32 accumulation;
-//          wh carries WH_BITS = 6 significant bits (below).  The dropped
-//          wl xl term is ~2^-19 and the weights keep 17 bits: measured
-//          normwise error 2e-6..3e-6, inside the fp32 path's 1e-5 contract.
+//          wh carries WH_BITS = 8 significant bits (below).  The dropped
+//          wl xl term is ~2^-21 and the weights keep 19 bits: inside the
+//          fp32 path's 1e-5 contract on every tested shape (below).
 //   BF16   one bf16 term (unscaled), fp32 accumulation (config C).
 //   F16    one scaled fp16 term.
 //
@@ -178,13 +178,14 @@ __device__ __forceinline__ void split_record(const float (&v)[CCH], float s,
 // then exact in fp16) and wl = fp16(w s - wh); WH_BITS = 11 would be the
 // plain fp16 hi/lo split (wh = fp16(w s)).  The decoder is power-bound and
 // its MFMA rate rises as the operands' bit density falls:
-// wh with 6 significant bits feeds two of the three MFMAs per product.  The
-// weights keep 6 + 11 = 17 bits, the dropped wl xl term is ~2^-17 of a
-// product.  Measured (profiles/r04j, A/B in one call): heads launch 111.6 /
-// 111.7 -> 108.3 / 108.5 ms (config B 448.0 / 446.4 -> 459.3 / 458.0
-// images/s; 8 bits: 109.9 ms); decoder-conv normwise error vs fp64 2.1e-6 ->
-// 3.0e-6 (contract 1e-5).
-constexpr int WH_BITS = 6;
+// wh feeds two of the three MFMAs per product.  8 bits: the weights keep
+// 8 + 11 = 19 bits, the dropped wl xl term is ~2^-21 of a product.
+// Measured (profiles/r04j): heads launch 111.6 / 111.7 -> 109.9 / 109.9 ms
+// (config B +1.3%); 6 bits was faster (108.3 ms, +2.6%) but left one random
+// module variant (k = 1 over 16 channels, heavy cancellation) at 1.33e-5
+// normwise against the 1e-5 contract; 8 bits: 1.5e-6 there and all 1200
+// cases of the deep random sweep green (profiles/r04wb).
+constexpr int WH_BITS = 8;
 
 template <int PREC>
 __device__ __forceinline__ void split_record_w(const float (&v)[CCH], float s,
