@@ -285,6 +285,9 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="initialise torch.distributed and run the reducer exchange even at one rank "
                          "(RCCL at world 1 on a 1-GPU box exercises the N>1 code path)")
+    ap.add_argument("--xcorr-split", type=int, default=None, choices=(0, 1),
+                    help="correlation of a mixed launch split by kernel per unit on two streams "
+                         "(TMREngine.xcorr_split; default: the engine's)")
     ap.add_argument("--no-xcorr-classes", action="store_true",
                     help="skip the per-template-class correlation launches after the timed region "
                          "(PMC passes: one launch per kernel role)")
@@ -367,6 +370,8 @@ def main():
     # per-kernel events, so the kernels' HIP-event times then come from one
     # eager step after the timed loop (same kernels, same stream)
     eng.use_graphs = not a.no_graphs
+    if a.xcorr_split is not None:
+        eng.xcorr_split = bool(a.xcorr_split)
     if a.path == "module":  # the module's engine replays each exemplar's forward
         model.engine().use_graphs = not a.no_graphs
     graphs = eng.use_graphs and (a.path == "module" or B * E <= eng.GRAPH_MAX_UNITS)
@@ -504,6 +509,9 @@ def main():
                           "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
                                                                      else ("f16", "scaled fp16")))
                        if xk == "mfma" else
+                       "tmr_xcorr_out split per unit: VALU (xcorr_rows_kernel) for the units the per-k cost "
+                       "model gives it, MFMA (xcorr_mfma_kernel, row-Toeplitz) for the rest, two streams"
+                       if xk == "split" else
                        "tmr_xcorr_prec VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
                       + " + /hw + pad + scale + max|f_TM|; kernel chosen by the measured per-k cost model "
                         "(engine.XCORR_COST)",

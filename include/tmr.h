@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 1
+#define TMR_ABI_VERSION 2  /* 2: per-unit out_absmax, per-sample activation scales */
 
 enum {
     TMR_OK = 0,
@@ -52,7 +52,10 @@ typedef struct tmr_unit {
     int64_t tmpl_offset;   /* float offset of this unit's [C,ht,wt] template      */
     int32_t row_offset;    /* sum of ht over the units before this one (the MFMA  */
                            /* correlation's split-template rows, tmr_template_split) */
-    int32_t pad_;
+    int32_t out_unit;      /* the correlation's output plane [out_unit][C][H][W], */
+                           /* out_absmax slot and split-template exponent row: the */
+                           /* unit's index in the full unit set (= its position,   */
+                           /* unless a launch covers a subset of the units)        */
 } tmr_unit_t;
 
 /* Per-unit peak-finder parameters (utils/TM_utils.py:236-278). */
@@ -90,12 +93,10 @@ int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *
  * squeeze!=0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and
  * `work` must hold U*C*H*W floats; otherwise out is [U,C,H,W] and work may
  * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79).
- * out_absmax (nullable, device float[TMR_ABSMAX_SLOTS]): the kernel raises
- * the slots so that max over slots >= max |out| (each workgroup's max goes to
- * one slot; spreading avoids same-address atomics); reduce them with
- * tmr_absmax(out_absmax, TMR_ABSMAX_SLOTS, ...) into the split decoder's
- * activation scale source, with no extra pass over out. */
-#define TMR_ABSMAX_SLOTS 256
+ * out_absmax (nullable, device float[U], zeroed by the caller): the kernel
+ * raises out_absmax[u] to max |out[u]| (one atomic per workgroup and unit),
+ * the split decoder's PER-UNIT activation scale source (tmr_split_xpack with
+ * xmax_per_sample, TMR_SPLIT_XMAX_PER_UNIT), with no extra pass over out. */
 int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
               const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
               const float *scale, int squeeze, float *out, float *relu_out, float *work,
@@ -154,7 +155,10 @@ int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templ
  * (C * row_offset(u) + c * ht * nk) * 2 + (i * nk + b) * 2 + k; then e
  * int32[U][C].  row_offset(u) = sum over earlier units of ht * nk(wt) and
  * total_rows = that sum over all units (tmr_unit_t.row_offset, set by the
- * host); size in bytes from tmr_template_split_size. */
+ * host); size in bytes from tmr_template_split_size.  The exponents are
+ * stored at row units[u].out_unit: a launch over a subset of a unit set
+ * (absolute row_offset / out_unit) fills that set's buffer, sized with the
+ * set's U and total_rows. */
 int64_t tmr_template_split_size(int U, int C, int64_t total_rows);
 int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
                        int64_t total_rows, void *out, void *stream);
@@ -195,9 +199,21 @@ int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int
  *   TMR_PREC_F16:   one scaled fp16 term.
  * tmr_absmax: *out = max(|x|) (or max(*out, |x|) when accumulate), the scale
  * source for the packs and the conv (F16X3 / F16; NULL allowed for BF16).
+ * tmr_absmax_rows: the same per sample, out[s] = max |x[s][0..n)| for
+ * x [S][n].  tmr_scale_merge: out_img[b] = max(img_max[b] (nullable: 0),
+ * unit_max[u] over the units with unit_image[u] == b), out_unit[u] =
+ * out_img[unit_image[u]] (out_img nullable) -- one scale per image for a
+ * launch whose tiles read an image's src0 records and its units' src1
+ * records together.
  * tmr_split_xpack: x [S][C][H][W] fp32 -> [S][ceil(C/32)*halves][Hp][Wp][64 B]
  * (halves 2 for F16X3: hi, lo), zero padded to whole 16x32 tiles plus the ks
- * halo (sizes in BYTES).
+ * halo (sizes in BYTES).  xmax_per_sample = 0: one scale source *xmax for
+ * every sample; 1: xmax[s] for sample s (float[S]); 2: xmax[s][y][x] per
+ * (output-resolution) pixel, for TMR_SPLIT_XMAX_PER_PIXEL 1x1 convs.
+ * Per-sample scales make a unit's arithmetic independent of the other units
+ * of the batch: its hi/lo parts never go subnormal because another sample is
+ * 2^20 larger (a power-of-two rescale is exact otherwise, so results equal
+ * the single-unit run's bit for bit).
  * tmr_split_wpack: w [N][C0+C1][ks][ks] -> [ks*ks][ceil(C0/32)+ceil(C1/32)]
  * [ceil(N/128)*128][rec]; the conv's src0 (per image, C0 channels, packed by
  * xpack with S = images) and src1 (per unit, C1) may both be present.
@@ -208,9 +224,12 @@ int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int
 #define TMR_PREC_BF16 1
 #define TMR_PREC_F16 2
 int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stream);
+int tmr_absmax_rows(const float *x, int S, int64_t n, int accumulate, float *out, void *stream);
+int tmr_scale_merge(const float *img_max, const float *unit_max, const int32_t *unit_image, int B, int U,
+                    float *out_img, float *out_unit, void *stream);
 int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec);
 int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
-                    const float *xmax, void *out, void *stream);
+                    const float *xmax, int xmax_per_sample, void *out, void *stream);
 /* tmr_split_xpack16: the TMR_PREC_BF16 records of a bf16 x [S][C][H][W]
  * (tmr_xcorr_out's bf16 f_TM; W % 8 == 0): bit-identical to tmr_split_xpack
  * of the fp32 values those bf16 elements round. */
@@ -224,7 +243,7 @@ int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int pre
  * Wd[n][k] b[k] per tap (matching_net.py:27-30,56,63-69), fp64 accumulation;
  * out [N][Cin+1][ks][ks] from wd [N][Cw][ks][ks] (first Cp channels = fp). */
 int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample, int ones,
-                       int ks, int prec, const float *xmax, void *out, void *stream);
+                       int ks, int prec, const float *xmax, int xmax_per_sample, void *out, void *stream);
 int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
                         const float *proj_b, int Cin, float *out, void *stream);
 int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec);
@@ -244,6 +263,20 @@ int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, con
  * contract; halves the heads launch's initial-value read) */
 #define TMR_SPLIT_OUT_BF16 8
 #define TMR_SPLIT_INIT_BF16 16
+/* xmax is float[U], one activation scale source per unit u (the output slab;
+ * the image index for a per-image store): both record sets a tile reads must
+ * have been packed with that unit's value (tmr_split_xpack xmax_per_sample,
+ * tmr_scale_merge when src0 is per image) */
+#define TMR_SPLIT_XMAX_PER_UNIT 32
+/* 1x1 plain stores (no acc_init, no tiled out): xmax is float[U][H][W], one
+ * scale source per output pixel -- the max over that pixel's input channels
+ * (tmr_pixel_absmax), the records packed with tmr_split_xpack(_up)
+ * xmax_per_sample = 2 -- so every pixel is fp32-grade relative to its own
+ * magnitude (the projection: templates cut from a quiet region of an image
+ * are renormalised by the correlation, template_matching.py:75,31) */
+#define TMR_SPLIT_XMAX_PER_PIXEL 64
+/* out[s][p] = max_c |x[s][c][p]| for x [S][C][HW] */
+int tmr_pixel_absmax(const float *x, int S, int C, int64_t HW, float *out, void *stream);
 int64_t tmr_split_acc_size(int U, int N, int H, int W);
 int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
                          int C1, int U, int H, int W, int ks, int prec, const void *wpack,

@@ -1,7 +1,7 @@
 # Round 4 first GPU call: (1) a clean checkout (git archive of HEAD, shipped
 # as clean_head.tar) builds and passes smoke() on the box with nothing from
 # the working tree; (2) the full -m gpu suite incl. the RCCL world-1 tests;
-# (3) bench B.  Run from the repo root: gpurun -- bash profiles/gpu_r04a.sh
+# (3) bench B.  Run from the repo root: gpurun -- bash profiles/archive/gpu_r04a.sh
 set -o pipefail
 mkdir -p gpurun_out/r04a
 export TMPDIR=/tmp

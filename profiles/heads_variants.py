@@ -16,6 +16,8 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
   xl2a     the correlation's A fragments all come from template row 0 (L1/L2-resident)
   wsparseN / tsparseN   decoder weights' / correlation templates' hi part at
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
+  imgmajor an image's 3 units innermost in the heads grid (acc0 tile reuse; a correct build
+           for 3 units per image)
   l2dma    every DMA re-reads the first chunk's halo / first step's weights:
            the same instruction stream with real operand data, but L2-resident
            (no MALL / HBM traffic)
@@ -90,6 +92,16 @@ def variant_source(name: str, src: str) -> str:
         src = _sub(src, "const uint32_t src = (uint32_t)(sgx * G::tps(px) + tl) * tapstride + (uint32_t)cx * a.Npad * WREC + wnt +",
                    "const uint32_t src = (uint32_t)tl * tapstride + wnt +")
         return src
+    if name == "imgmajor":  # an image's E = 3 units innermost in the block order
+        # (correct results for U % 3 == 0 with 3 units per image, e.g. config B): the 3 blocks of an
+        # image at one (pixel tile, channel tile) are consecutive on one XCD, so its acc0 tile is
+        # fetched from HBM once and served from L2 to the other two
+        return _sub(src, """        const int per_unit = a.NT * a.MT;
+        u = L / per_unit;
+        const int r = L - u * per_unit;""", """        const int per_unit = a.NT * a.MT;
+        const int ub = L / (3 * per_unit), rr = L - ub * 3 * per_unit;
+        u = ub * 3 + rr % 3;
+        const int r = rr / 3;""")
     raise SystemExit(f"unknown variant {name}")
 
 

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 kernel-trace database (run_results.db) into the
 per-kernel table committed under profiles/ (calls, total, average, share).
 
-    python profiles/summarize.py gpurun_out/prof_r1a/run_results.db > profiles/r01_kernel_stats.md
+    python profiles/summarize.py gpurun_out/prof_r1a/run_results.db > profiles/archive/r01_kernel_stats.md
 """
 import sqlite3
 import sys

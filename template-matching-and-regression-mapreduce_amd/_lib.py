@@ -24,10 +24,10 @@ _lib = None
 
 # ABI structs (must match include/tmr.h)
 UNIT_DTYPE = np.dtype({
-    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset", "row_offset"],
+    "names": ["image", "type", "ht", "wt", "roi", "pbox", "tmpl_offset", "row_offset", "out_unit"],
     "formats": [np.int32, np.int32, np.int32, np.int32, (np.float32, 4), (np.int32, 4), np.int64,
-                np.int32],
-    "offsets": [0, 4, 8, 12, 16, 32, 48, 56],
+                np.int32, np.int32],
+    "offsets": [0, 4, 8, 12, 16, 32, 48, 56, 60],
     "itemsize": 64,
 })
 PEAK_DTYPE = np.dtype({
@@ -44,6 +44,8 @@ TEMPLATE_PROTOTYPE = 1
 PREC_CODES = {"fp32": 0, "bf16": 1, "f16": 2}
 SPLIT_TILED_OUT, SPLIT_TILED_INIT, SPLIT_INIT_BCAST = 1, 2, 4
 SPLIT_OUT_BF16, SPLIT_INIT_BF16 = 8, 16  # one-term precisions: bf16 acc0 slabs
+SPLIT_XMAX_PER_UNIT = 32  # xmax is float[U]: one activation scale per unit / output slab
+SPLIT_XMAX_PER_PIXEL = 64  # 1x1 stores: xmax is float[U][H][W], one scale per output pixel
 # correlation kernel choice (tmr_xcorr_algo)
 XCORR_ALGOS = {"auto": 0, "valu": 1, "mfma": 2}
 
@@ -71,10 +73,13 @@ SIGNATURES = {
     "tmr_heads_partials_size": (_L, [_I, _I, _I, _I]),
     "tmr_heads_reduce": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "tmr_absmax": (_I, [_P, _L, _I, _P, _P]),
+    "tmr_absmax_rows": (_I, [_P, _I, _L, _I, _P, _P]),
+    "tmr_scale_merge": (_I, [_P, _P, _P, _I, _I, _P, _P, _P]),
+    "tmr_pixel_absmax": (_I, [_P, _I, _I, _L, _P, _P]),
     "tmr_split_xpack_size": (_L, [_I, _I, _I, _I, _I, _I]),
-    "tmr_split_xpack": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_xpack": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P]),
     "tmr_split_xpack16": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
-    "tmr_split_xpack_up": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "tmr_split_xpack_up": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P]),
     "tmr_split_fold_proj": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _P, _P]),
     "tmr_split_wpack_size": (_L, [_I, _I, _I, _I, _I]),
     "tmr_split_wpack": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -116,7 +121,7 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.tmr_version() != 1:
+        if lib.tmr_version() != 2:
             raise TMRError("libtmr.so ABI version mismatch")
         _lib = lib
         return lib

@@ -60,9 +60,9 @@ typedef __bf16 b4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
 
 // Measured and dropped (code in git history): register-staged operand loads
-// (buffer_load + ds_write instead of LDS-DMA; 3.7% slower, profiles/r02p_*),
+// (buffer_load + ds_write instead of LDS-DMA; 3.7% slower, profiles/archive/r02p_*),
 // initial values read inside the main loop (slower: a load issued in a step
-// is forced by that step's in-order vmcnt wait; profiles/r02ai, r02aj), the
+// is forced by that step's in-order vmcnt wait; profiles/archive/r02ai, r02aj), the
 // next step's first B fragments read before the step barrier (4% slower,
 // r02an), wave priority over the MFMA stream (no change, r02av).
 
@@ -113,14 +113,17 @@ template <> struct Prec<TMR_PREC_F16> {
     typedef h8 V;
 };
 
-// power-of-two scale with max |x| * s < 2^14 (fp16 max 65504)
+// power-of-two scale with max |x| * s < 2^14 (fp16 max 65504), clamped to
+// [2^-63, 2^63] so that the product of an activation and a weight scale
+// stays a normal fp32 number (sources below 2^-49 or above 2^77 are then
+// scaled less than their range would allow)
 __device__ __forceinline__ float split_scale(const float *m) {
     if (!m) return 1.0f;
     const float v = *m;
     if (!(v > 0.0f && v <= 3.0e38f)) return 1.0f;
     int e;
     frexpf(v, &e);  // v < 2^e
-    return ldexpf(1.0f, 14 - e);
+    return ldexpf(1.0f, min(max(14 - e, -63), 63));
 }
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n
@@ -421,14 +424,20 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     // the exact power of two s_x s_w); masked elements read a clamped legal
     // address and are zeroed by a select, never by a branch around the load.
     // 16x16 accumulator: column = pixel l16, row = n 4*kg + r.
-    const float sxw = PR::SCALED ? split_scale(a.xmax) * split_scale(a.wmax) : 1.0f;
+    // activation scale: one per launch, or per unit / output slab u
+    // (TMR_SPLIT_XMAX_PER_UNIT: a unit's precision then does not depend on
+    // the magnitudes of the other units in the batch)
+    // (TMR_SPLIT_XMAX_PER_PIXEL: the epilogue undoes a scale per output pixel)
+    const float *xm = (a.xmax && !(a.flags & TMR_SPLIT_XMAX_PER_PIXEL))
+                          ? a.xmax + ((a.flags & TMR_SPLIT_XMAX_PER_UNIT) ? u : 0) : nullptr;
+    const float sxw = PR::SCALED ? split_scale(xm) * split_scale(a.wmax) : 1.0f;
     const int HW = a.H * a.W;
     f32x4 acc[NIN][8];
     // tiled acc layout: [slab][nt][mt][wave][in*8+jp][lane][4] fp32 (bf16
     // slabs: 8 B per 16-B group index), i.e. each accumulator register set is
     // one contiguous KB per wave (no masking).  Read before the main loop: the
     // blocks run in lockstep, so this is a chip-wide burst while no MFMA runs
-    // (12% of the one-term kernel with fp32 slabs, profiles/r02ah_*; halved
+    // (12% of the one-term kernel with fp32 slabs, profiles/archive/r02ah_*; halved
     // by the bf16 slab of the bf16 contract)
     const int islab = (a.flags & TMR_SPLIT_INIT_BCAST) ? 0 : img;  // acc_init slab
     const size_t tile_off = ((((size_t)islab * a.NT + nt) * a.MT + mt) * NWAVES + wave) * ACCW;
@@ -660,6 +669,17 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
         for (int e = tid; e < BM * NHEAD; e += NTHREADS) shw[e] = a.headw[(size_t)nt * BM * NHEAD + e];
     __syncthreads();
     if constexpr (EPI == 0) {
+        // TMR_SPLIT_XMAX_PER_PIXEL (1x1 convs): each accumulator column is one
+        // pixel, packed with its own scale (the max over its channels), so
+        // every output pixel is fp32-grade relative to its own magnitude
+        float invp[8];
+#pragma unroll
+        for (int jp = 0; jp < 8; ++jp) {
+            invp[jp] = inv;
+            const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
+            if (PR::SCALED && (a.flags & TMR_SPLIT_XMAX_PER_PIXEL) && y < a.H && x < a.W)
+                invp[jp] = 1.0f / (split_scale(a.xmax + ((size_t)u * a.H + y) * a.W + x) * split_scale(a.wmax));
+        }
 #pragma unroll
         for (int in = 0; in < NIN; ++in)
 #pragma unroll
@@ -671,7 +691,7 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
 #pragma unroll
                 for (int jp = 0; jp < 8; ++jp) {
                     const int y = ty0 + wpix * 4 + (jp >> 1), x = tx0 + (jp & 1) * 16 + l16;
-                    float v = acc[in][jp][r] * inv + bn;
+                    float v = acc[in][jp][r] * invp[jp] + bn;
                     if (a.leaky) v = v >= 0.0f ? v : v * 0.01f;
                     if (nin && y < a.H && x < a.W) a.out[((size_t)u * a.N + n) * HW + (size_t)y * a.W + x] = v;
                 }
@@ -837,6 +857,63 @@ __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4 *__restric
     absmax_commit(m, out);
 }
 
+// per-sample max |x| (tmr_absmax_rows): row s = blockIdx.y, blocks along x
+// stride over it; one atomic per block (absmax_commit)
+__global__ __launch_bounds__(256) void absmax_rows_kernel(const float *__restrict__ x, int64_t n, int vec,
+                                                          unsigned *__restrict__ out) {
+    const float *xr = x + (size_t)blockIdx.y * n;
+    float m = 0.0f;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    if (vec) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(xr);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += step) {
+            const float4 v = x4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step)
+            m = fmaxf(m, fabsf(xr[i]));
+    }
+    absmax_commit(m, out + blockIdx.y);
+}
+
+// tmr_pixel_absmax: out[s][p] = max_c |x[s][c][p]| (one thread per pixel,
+// channel planes read in turn: coalesced across the wave's pixels)
+__global__ __launch_bounds__(256) void pixel_absmax_kernel(const float *__restrict__ x, int S, int C, int64_t HW,
+                                                           float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)S * HW) return;
+    const int64_t s = i / HW, p = i - s * HW;
+    const float *xp = x + (size_t)s * C * HW + p;
+    float m = 0.0f;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, fabsf(xp[(size_t)c * HW]));
+    out[i] = m;
+}
+
+// tmr_scale_merge: block b finds its image's units (unit_image[u] == b),
+// out_img[b] = max(img_max[b], their unit_max), then writes that to each
+// of them in out_unit (the shared scale of a launch whose tiles read the
+// image's records and the unit's records together)
+__global__ __launch_bounds__(256) void scale_merge_kernel(const float *__restrict__ img_max,
+                                                          const float *__restrict__ unit_max,
+                                                          const int32_t *__restrict__ unit_image, int U,
+                                                          float *__restrict__ out_img,
+                                                          float *__restrict__ out_unit) {
+    __shared__ float red[4];
+    const int b = blockIdx.x;
+    float m = 0.0f;
+    for (int u = threadIdx.x; u < U; u += blockDim.x)
+        if (unit_image[u] == b) m = fmaxf(m, unit_max[u]);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (img_max) m = fmaxf(m, img_max[b]);
+    if (threadIdx.x == 0 && out_img) out_img[b] = m;
+    for (int u = threadIdx.x; u < U; u += blockDim.x)
+        if (unit_image[u] == b) out_unit[u] = m;
+}
+
 // Activation records: value v(s, ch, y, x) -> [S][NCc*HALVES][4 pieces][Hp][Wp][16 B],
 // padded (yp, xp) holding v at (yp - ks/2, xp - ks/2), zero outside.  One
 // thread per (s, chunk, yp, xp) writes the chunk's hi (and lo) record.
@@ -847,7 +924,8 @@ __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4 *__restric
 template <int PREC, int MODE>
 __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hin, int Win, int ups,
                              int ones, int H, int W, int NCc, int Hp, int Wp, int pad,
-                             const float *__restrict__ xmax, typename Prec<PREC>::V *__restrict__ out) {
+                             const float *__restrict__ xmax, int xms,
+                             typename Prec<PREC>::V *__restrict__ out) {
     constexpr int HALVES = Prec<PREC>::HALVES;
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -860,7 +938,11 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
     const int s = (int)(r / NCc);
     const int y = yp - pad, xx = xp - pad;
     const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
-    const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
+    // scale source: one (xms 0), per sample (1) or per output pixel (2: [S][H][W])
+    const float *xm = !xmax ? nullptr
+                      : xms == 2 ? (in ? xmax + ((size_t)s * H + y) * W + xx : nullptr)
+                                 : xmax + (size_t)s * xms;
+    const float sc = Prec<PREC>::SCALED ? split_scale(xm) : 1.0f;
     float v[CCH];
 #pragma unroll
     for (int k = 0; k < CCH; ++k) {
@@ -907,7 +989,7 @@ constexpr int XPACK16_RPB = 4;  // rows per block of the bf16-input record pack 
 template <int PREC, typename IN = float, int RPB = 1>
 __global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, int S, int Cin, int H, int W,
                                                      int NCc, int Hp, int Wp, int pad, int64_t nseg,
-                                                     int64_t nbord, const float *__restrict__ xmax,
+                                                     int64_t nbord, const float *__restrict__ xmax, int xms,
                                                      typename Prec<PREC>::V *__restrict__ out) {
     constexpr int HALVES = Prec<PREC>::HALVES;
     typedef typename Prec<PREC>::V V;
@@ -939,7 +1021,7 @@ __global__ __launch_bounds__(256) void xpack4_kernel(const IN *__restrict__ x, i
             *reinterpret_cast<INV *>(&tile[rr][ch][VE * xv]) = v;
         }
         __syncthreads();
-        const float sc = Prec<PREC>::SCALED ? split_scale(xmax) : 1.0f;
+        const float sc = Prec<PREC>::SCALED ? split_scale(xmax ? xmax + (size_t)s * xms : nullptr) : 1.0f;
         V *o = out + ((size_t)s * NCc + c) * HALVES * P * plane + (size_t)(y0 + pad) * Wp + x0 + pad;
 #pragma unroll
         for (int k = 0; k < RPB * XSEG * P / 256; ++k) {
@@ -1062,6 +1144,10 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     TMR_REQUIRE(!(flags & (TMR_SPLIT_OUT_BF16 | TMR_SPLIT_INIT_BF16)) || prec != TMR_PREC_F16X3);
     TMR_REQUIRE(!(flags & TMR_SPLIT_OUT_BF16) || (flags & TMR_SPLIT_TILED_OUT));
     TMR_REQUIRE(!(flags & TMR_SPLIT_INIT_BF16) || (flags & TMR_SPLIT_TILED_INIT));
+    // per-pixel activation scales: 1x1 plain stores only (the K dimension of a
+    // kxk conv mixes neighbouring pixels; the scale is undone in that epilogue)
+    TMR_REQUIRE(!(flags & TMR_SPLIT_XMAX_PER_PIXEL) ||
+                (ks == 1 && !epi && !acc_init && !(flags & (TMR_SPLIT_TILED_OUT | TMR_SPLIT_XMAX_PER_UNIT))));
     SArgs a = {};
     a.x0 = static_cast<const char *>(xp0);
     a.x1 = static_cast<const char *>(xp1);
@@ -1094,7 +1180,7 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
 
 template <int MODE>
 int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int ones, int H, int W,
-                 int ks, int prec, const float *xmax, void *out, void *stream) {
+                 int ks, int prec, const float *xmax, int xms, void *out, void *stream) {
     const int C = Cin + (MODE == 1 && ones ? 1 : 0);
     const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
     const int64_t total = (int64_t)S * NCc * Hp * Wp;
@@ -1103,17 +1189,17 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
     // one-term records from LDS-transposed row segments (bf16 0.61 -> 0.50 ms
     // per 48 units at 128^2, r02bo3); the 3-term records stay on the
     // one-pixel kernel (0.61 vs 0.73 ms: twice the stores per staged byte)
-    if (MODE == 0 && W % 4 == 0 && prec != TMR_PREC_F16X3) {
+    if (MODE == 0 && W % 4 == 0 && prec != TMR_PREC_F16X3 && xms != 2) {
         const int64_t nseg = (int64_t)S * NCc * H * tmr_cdiv(W, XSEG), nbord = (int64_t)Hp * Wp - (int64_t)H * W;
         const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
         switch (prec) {
             case TMR_PREC_BF16:
                 hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_BF16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
-                                   ks / 2, nseg, nbord, nullptr, static_cast<b8 *>(out));
+                                   ks / 2, nseg, nbord, nullptr, 0, static_cast<b8 *>(out));
                 break;
             default:
                 hipLaunchKernelGGL(xpack4_kernel<TMR_PREC_F16>, g4, blk, 0, s, x, S, Cin, H, W, NCc, Hp, Wp,
-                                   ks / 2, nseg, nbord, xmax, static_cast<h8 *>(out));
+                                   ks / 2, nseg, nbord, xmax, xms, static_cast<h8 *>(out));
                 break;
         }
         TMR_CHECK_LAUNCH();
@@ -1122,15 +1208,15 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
     switch (prec) {
         case TMR_PREC_F16X3:
             hipLaunchKernelGGL((xpack_kernel<TMR_PREC_F16X3, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
-                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, xms, static_cast<h8 *>(out));
             break;
         case TMR_PREC_BF16:
             hipLaunchKernelGGL((xpack_kernel<TMR_PREC_BF16, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
-                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, nullptr, static_cast<b8 *>(out));
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, nullptr, 0, static_cast<b8 *>(out));
             break;
         default:
             hipLaunchKernelGGL((xpack_kernel<TMR_PREC_F16, MODE>), grid, blk, 0, s, x, S, Cin, Hin, Win,
-                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, static_cast<h8 *>(out));
+                               ups, ones, H, W, NCc, Hp, Wp, ks / 2, xmax, xms, static_cast<h8 *>(out));
             break;
     }
     TMR_CHECK_LAUNCH();
@@ -1158,16 +1244,50 @@ extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out,
     return TMR_OK;
 }
 
+extern "C" int tmr_absmax_rows(const float *x, int S, int64_t n, int accumulate, float *out, void *stream) {
+    TMR_REQUIRE(out && S > 0 && S < 65536 && n >= 0 && (n == 0 || x));
+    hipStream_t s = tmr_stream(stream);
+    if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * (size_t)S, s) != hipSuccess) return TMR_E_HIP;
+    if (n == 0) return TMR_OK;
+    const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0;
+    const int64_t per = vec ? n / 4 : n;
+    // about 2048 blocks in all, >= 8 elements per thread
+    const int bpr = (int)std::max<int64_t>(1, std::min<int64_t>(tmr_cdiv(per, 256 * 8), std::max(1, 2048 / S)));
+    hipLaunchKernelGGL(absmax_rows_kernel, dim3(bpr, S), dim3(256), 0, s, x, n, vec,
+                       reinterpret_cast<unsigned *>(out));
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_pixel_absmax(const float *x, int S, int C, int64_t HW, float *out, void *stream) {
+    TMR_REQUIRE(x && out && S > 0 && C > 0 && HW > 0);
+    const int64_t n = (int64_t)S * HW;
+    hipLaunchKernelGGL(pixel_absmax_kernel, dim3((unsigned)tmr_cdiv(n, 256)), dim3(256), 0, tmr_stream(stream), x,
+                       S, C, HW, out);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_scale_merge(const float *img_max, const float *unit_max, const int32_t *unit_image, int B,
+                               int U, float *out_img, float *out_unit, void *stream) {
+    TMR_REQUIRE(unit_max && unit_image && out_unit && B > 0 && U > 0 && B < (1 << 24));
+    hipLaunchKernelGGL(scale_merge_kernel, dim3(B), dim3(256), 0, tmr_stream(stream), img_max, unit_max,
+                       unit_image, U, out_img, out_unit);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
 extern "C" int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec) {
     if (S <= 0 || C <= 0 || H <= 0 || W <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
     return (int64_t)S * tmr_cdiv(C, CCH) * prec_halves(prec) * pad_h(H, ks) * pad_w(W, ks) * XREC;
 }
 
 extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
-                               const float *xmax, void *out, void *stream) {
+                               const float *xmax, int xmax_per_sample, void *out, void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
-    return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, out, stream);
+    TMR_REQUIRE(xmax_per_sample >= 0 && xmax_per_sample <= 2);
+    return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, xmax_per_sample, out, stream);
 }
 
 extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
@@ -1180,20 +1300,21 @@ extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int 
     const int64_t nbord = (int64_t)Hp * Wp - (int64_t)H * W;
     const dim3 g4((unsigned)(nseg + tmr_cdiv(nbord * S * NCc, 256)));
     hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16, __bf16, RPB>), g4, dim3(256), 0, tmr_stream(stream),
-                       static_cast<const __bf16 *>(x), S, C, H, W, NCc, Hp, Wp, ks / 2, nseg, nbord, nullptr,
+                       static_cast<const __bf16 *>(x), S, C, H, W, NCc, Hp, Wp, ks / 2, nseg, nbord, nullptr, 0,
                        static_cast<b8 *>(out));
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
 
 extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample,
-                                  int ones, int ks, int prec, const float *xmax, void *out,
-                                  void *stream) {
+                                  int ones, int ks, int prec, const float *xmax, int xmax_per_sample,
+                                  void *out, void *stream) {
     TMR_REQUIRE(f && out && S > 0 && Cin > 0 && Hin > 0 && Win > 0 && ks_ok(ks) && prec_ok(prec));
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
+    TMR_REQUIRE(xmax_per_sample >= 0 && xmax_per_sample <= 2);
     const int H = upsample ? 2 * Hin : Hin, W = upsample ? 2 * Win : Win;
     return xpack_launch<1>(f, S, Cin, Hin, Win, upsample ? 1 : 0, ones ? 1 : 0, H, W, ks, prec, xmax,
-                           out, stream);
+                           xmax_per_sample, out, stream);
 }
 
 extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,

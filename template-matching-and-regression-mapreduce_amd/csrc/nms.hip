@@ -10,17 +10,28 @@
 //   sort   : rocprim segmented radix sort of (score, index) pairs, descending
 //            and stable: ties keep the lower index first, as torchvision's
 //            stable sort (O(n log) per image instead of O(n^2) rank counting)
-//   strips : the 64-bit IoU suppression words of a STRIP of S row blocks
-//            (64 sorted rows each) against every later column block are
-//            computed (mask_strip) and consumed (reduce_strip) strip after
-//            strip.  One workgroup per image keeps the running "removed"
-//            bitmap (one bit per sorted row, in LDS, parked in HBM between
-//            strips): a row block's in-block greedy chain is resolved from
-//            registers (readlane over the surviving rows), then its kept
-//            rows' words are OR-ed into the later blocks by all its threads.  Memory is O(n) per image plus ONE strip buffer whose
-//            size is bounded (TMR_NMS_STRIP_WORDS) independently of n^2; the
-//            keep list equals the sequential torchvision loop because IoU(i,j)
-//            is bitwise symmetric and suppression only flows from kept rows.
+//   bins   : the sorted boxes are binned by their top-left corner on a
+//            per-image grid (<= 64 x 64 cells); two boxes can only overlap
+//            (and so only suppress, for iou_threshold >= 0) when each one's
+//            corner lies within the other's extent + the image's largest box
+//            extent, so a box's partners are found in a small window of cells
+//   pairs  : one thread per box, in cell order (neighbours in a wave scan the
+//            same cells): the exact IoU against every later-sorted box of its
+//            window; suppressions inside its own 64-row block go to a
+//            diagonal word, later ones to a list of up to CAP entries
+//   greedy : one wave per image walks the 64-row blocks in score order: the
+//            block's chain is resolved from the diagonal words in registers,
+//            the kept rows' lists are OR-ed into the image's "removed" bitmap
+//            in LDS (a kept row with more than CAP partners rescans its
+//            window instead).  Memory is O(candidates); the work is the
+//            spatial pairs, not n^2/2 (round 4's dense strips: 4.3e9 IoU
+//            pairs per config-E step, 2.9 ms of mask + 2.0 ms of strip
+//            reduction).  The keep list equals the sequential torchvision
+//            loop: IoU(i, j) is evaluated with the same expression, pairs
+//            outside a window have no intersection (ovr = 0 or NaN, never
+//            > a threshold >= 0), and suppression only flows from kept rows.
+//            A negative threshold or a non-finite box puts the image in ONE
+//            cell (every pair evaluated).
 // Built with -ffp-contract=off.
 #include <algorithm>
 
@@ -30,11 +41,16 @@
 
 namespace {
 
-// strip buffer budget: 32 Mi 64-bit words (256 MiB) across all images of a
-// call; a strip holds S row blocks of every image (S >= 1)
-constexpr int64_t STRIP_WORDS = 32ll << 20;
 // rocprim's temporary storage beyond its key/value double buffers
 constexpr int64_t SORT_SLACK = 1 << 20;
+constexpr int GB = 64;            // bins per axis (at most)
+constexpr int NCELL = GB * GB;
+constexpr int CAP = 32;           // listed later-block suppressions per row
+
+struct BinHdr {
+    float x0, y0, icx, icy, wmax, hmax;
+    int gx, gy;
+};
 
 struct NmsWork {
     float *s;        // [T] scores (unit order)
@@ -43,10 +59,16 @@ struct NmsWork {
     float *r;        // [T][2]
     int32_t *idx;    // [T] local row index (sort values in)
     int32_t *order;  // [T] sorted position -> local index
-    float *sb;       // [T][4] boxes in sorted order (the strips' row and column operands)
-    uint64_t *removed;  // [sum_nb] running suppression bitmap per image
-    uint64_t *strip;    // [strip_words]
-    char *temp;         // rocprim temporary storage
+    float *sb;       // [T][4] boxes in sorted order
+    BinHdr *hdr;     // [G]
+    int32_t *cnt;    // [G][NCELL] per-cell counts, then fill cursors
+    int32_t *cst;    // [G][NCELL + 1] cell starts (local)
+    int32_t *clist;  // [T] sorted positions in cell order
+    float *cbox;     // [T][4] their boxes
+    uint64_t *diag;  // [T] in-block suppression word of each sorted row
+    int32_t *lcnt;   // [T] later-block suppressions of each sorted row
+    int32_t *lst;    // [T][CAP] the first CAP of them (sorted positions)
+    char *temp;      // rocprim temporary storage
     int64_t temp_bytes;
 };
 
@@ -54,13 +76,7 @@ __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_
 
 inline int64_t sort_temp_bound(int64_t T, int G) { return 8 * T + SORT_SLACK + 64 * (int64_t)(G + 1); }
 
-// S (row blocks per strip) and the strip buffer's words for these sizes
-inline void strip_plan(int64_t sum_nb, int64_t max_nb, int64_t &S, int64_t &words) {
-    S = std::max<int64_t>(1, std::min<int64_t>(max_nb, STRIP_WORDS / std::max<int64_t>(1, 64 * sum_nb)));
-    words = S * 64 * sum_nb;
-}
-
-inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int64_t strip_words, int G) {
+inline NmsWork carve(void *work, int64_t T, int G) {
     NmsWork w;
     char *p = (char *)work;
     w.s = (float *)p; p += align256(sizeof(float) * T);
@@ -70,15 +86,21 @@ inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int64_t strip_words,
     w.idx = (int32_t *)p; p += align256(sizeof(int32_t) * T);
     w.order = (int32_t *)p; p += align256(sizeof(int32_t) * T);
     w.sb = (float *)p; p += align256(sizeof(float) * 4 * T);
-    w.removed = (uint64_t *)p; p += align256(sizeof(uint64_t) * sum_nb);
-    w.strip = (uint64_t *)p; p += align256(sizeof(uint64_t) * strip_words);
+    w.hdr = (BinHdr *)p; p += align256(sizeof(BinHdr) * G);
+    w.cnt = (int32_t *)p; p += align256(sizeof(int32_t) * NCELL * (size_t)G);
+    w.cst = (int32_t *)p; p += align256(sizeof(int32_t) * (NCELL + 1) * (size_t)G);
+    w.clist = (int32_t *)p; p += align256(sizeof(int32_t) * T);
+    w.cbox = (float *)p; p += align256(sizeof(float) * 4 * T);
+    w.diag = (uint64_t *)p; p += align256(sizeof(uint64_t) * T);
+    w.lcnt = (int32_t *)p; p += align256(sizeof(int32_t) * T);
+    w.lst = (int32_t *)p; p += align256(sizeof(int32_t) * CAP * T);
     w.temp = p;
     w.temp_bytes = sort_temp_bound(T, G);
     return w;
 }
 
-inline int64_t work_bytes(int64_t T, int64_t sum_nb, int64_t strip_words, int G) {
-    const NmsWork w = carve(nullptr, T, sum_nb, strip_words, G);
+inline int64_t work_bytes(int64_t T, int G) {
+    const NmsWork w = carve(nullptr, T, G);
     return (int64_t)(w.temp - (char *)nullptr) + w.temp_bytes + 256;
 }
 
@@ -116,8 +138,8 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
     }
 }
 
-// Boxes in sorted order, once per call: the strips then read rows and
-// columns contiguously instead of through the order indirection.
+// Boxes in sorted order, once per call: the bins and pairs then read rows
+// contiguously instead of through the order indirection.
 __global__ void sort_boxes_kernel(const int64_t *__restrict__ cand_off, int G, NmsWork w) {
     const int g = blockIdx.y;
     const int64_t off = cand_off[g];
@@ -128,126 +150,232 @@ __global__ void sort_boxes_kernel(const int64_t *__restrict__ cand_off, int G, N
     }
 }
 
-// IoU words of row block ib = s*S + blockIdx.y (64 sorted rows, one per lane)
-// x column blocks jb0 .. jb0 + NJ - 1 (those >= ib): bit k of word (i, jb) =
-// IoU(row i, column jb*64 + k) > thr for columns after i.  A block of MW
-// waves shares the row block: wave w computes column blocks jb0 + w, jb0 + w
-// + MW, ... with the column boxes staged in LDS (read as broadcasts); the
-// NJ words of each row are then written row-contiguously through an LDS
-// transpose (8 rows x 64 B per store instruction instead of 64 scattered 8-B
-// words per column block), and blocks wholly below the diagonal exit first.
-constexpr int NJ = 8, MW = 4;
+// the IoU test of torchvision's CPU kernel (fp32 IoU, `(double)ovr > thr`);
+// with `prune` (thr >= 0) a pair without intersection is decided without
+// the division: ovr is then 0 or NaN, never > thr
+__device__ __forceinline__ bool iou_over(float4 bi, float ai, float4 bj, float aj, double thr, bool prune) {
+    const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+    const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+    float ww = xx2 - xx1, hh = yy2 - yy1;
+    ww = ww > 0.0f ? ww : 0.0f;
+    hh = hh > 0.0f ? hh : 0.0f;
+    const float inter = ww * hh;
+    if (prune && !(inter > 0.0f)) return false;
+    const float ovr = inter / (ai + aj - inter);
+    return (double)ovr > thr;
+}
 
-__global__ __launch_bounds__(64 * MW) void mask_strip_kernel(const int64_t *__restrict__ cand_off,
-                                                             const int64_t *__restrict__ nb_off, double thr,
-                                                             int64_t S, int64_t s, NmsWork w) {
-    __shared__ float4 cb[NJ * 64];
-    __shared__ float ca[NJ * 64];
-    __shared__ uint64_t tw[64][NJ + 1];
-    const int g = blockIdx.z;
-    const int64_t ib = s * S + blockIdx.y;
+__device__ __forceinline__ float box_area(float4 b) { return (b.z - b.x) * (b.w - b.y); }
+
+// per image: the grid over the boxes' top-left corners (x1, y1).  Cells are
+// at least 2^-16 of the coordinates' magnitude wide, so the one-cell slack of
+// the windows covers the fp32 rounding of the cell arithmetic; a non-finite
+// coordinate or a negative threshold gives one cell (every pair evaluated).
+__global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restrict__ cand_off, double thr,
+                                                        NmsWork w) {
+    __shared__ float red[6][4];
+    __shared__ int bad[4];
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
-    const int nb = (n + 63) / 64;
-    const int jb0 = blockIdx.x * NJ;
-    if (ib >= nb || jb0 >= nb || jb0 + NJ <= ib) return;  // block-uniform
-    const int tid = threadIdx.x, t = tid & 63, wv = tid >> 6;
-    const int jlo = max(jb0, (int)ib), jhi = min(jb0 + NJ, nb);  // column blocks of this block
     const float4 *sb = reinterpret_cast<const float4 *>(w.sb) + off;
-    for (int e = tid; e < (jhi - jlo) * 64; e += 64 * MW) {
-        const int j = jlo * 64 + e;
-        if (j < n) {
-            const float4 bj = sb[j];
-            cb[e] = bj;
-            ca[e] = (bj.z - bj.x) * (bj.w - bj.y);
-        }
+    float v[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, 0.0f, 0.0f};  // x1 min, y1 min, x1 max, y1 max, w, h
+    int nf = 0;
+    for (int p = tid; p < n; p += 256) {
+        const float4 bb = sb[p];
+        nf |= !(isfinite(bb.x) && isfinite(bb.y) && isfinite(bb.z) && isfinite(bb.w));
+        v[0] = fminf(v[0], bb.x); v[1] = fminf(v[1], bb.y);
+        v[2] = fmaxf(v[2], bb.x); v[3] = fmaxf(v[3], bb.y);
+        v[4] = fmaxf(v[4], bb.z - bb.x); v[5] = fmaxf(v[5], bb.w - bb.y);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        v[0] = fminf(v[0], __shfl_xor(v[0], o)); v[1] = fminf(v[1], __shfl_xor(v[1], o));
+        v[2] = fmaxf(v[2], __shfl_xor(v[2], o)); v[3] = fmaxf(v[3], __shfl_xor(v[3], o));
+        v[4] = fmaxf(v[4], __shfl_xor(v[4], o)); v[5] = fmaxf(v[5], __shfl_xor(v[5], o));
+        nf |= __shfl_xor(nf, o);
+    }
+    if (lane == 0) {
+        for (int k = 0; k < 6; ++k) red[k][wv] = v[k];
+        bad[wv] = nf;
     }
     __syncthreads();
-    const int i = (int)ib * 64 + t;
-    const float4 bi = i < n ? sb[i] : float4{0.0f, 0.0f, 0.0f, 0.0f};
-    const float ai = (bi.z - bi.x) * (bi.w - bi.y);
-    for (int jb = jlo + wv; jb < jhi; jb += MW) {
-        uint64_t bits = 0;
-        const int kmax = min(64, n - jb * 64);
-        const int kmin = jb == ib ? t + 1 : 0;  // columns after row i only
-        const int base = (jb - jlo) * 64;
-#pragma unroll 4
-        for (int k = 0; k < kmax; ++k) {
-            const float4 bj = cb[base + k];
-            const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
-            const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
-            float ww = xx2 - xx1, hh = yy2 - yy1;
-            ww = ww > 0.0f ? ww : 0.0f;
-            hh = hh > 0.0f ? hh : 0.0f;
-            const float inter = ww * hh;
-            const float ovr = inter / (ai + ca[base + k] - inter);
-            if (k >= kmin && (double)ovr > thr) bits |= (1ull << k);
-        }
-        tw[t][jb - jb0] = i < n ? bits : 0ull;
+    if (tid != 0) return;
+    for (int q = 1; q < 4; ++q) {
+        v[0] = fminf(v[0], red[0][q]); v[1] = fminf(v[1], red[1][q]);
+        v[2] = fmaxf(v[2], red[2][q]); v[3] = fmaxf(v[3], red[3][q]);
+        v[4] = fmaxf(v[4], red[4][q]); v[5] = fmaxf(v[5], red[5][q]);
+        nf |= bad[q];
     }
-    __syncthreads();
-    // strip layout per image: [S*64 rows][nb words]; lanes (8 rows x 8 words)
-    uint64_t *dst = w.strip + S * 64 * nb_off[g] + (int64_t)(blockIdx.y * 64) * nb;
-    const int wq = t & 7, rq = t >> 3;
-    const int jb = jb0 + wq;
-    for (int r0 = 8 * wv; r0 < 64; r0 += 8 * MW) {
-        const int r = r0 + rq;
-        if (jb >= jlo && jb < jhi && (int)ib * 64 + r < n) dst[(int64_t)r * nb + jb] = tw[r][wq];
+    BinHdr h;
+    h.x0 = v[0]; h.y0 = v[1];
+    h.wmax = v[4]; h.hmax = v[5];
+    h.gx = h.gy = 1;
+    h.icx = h.icy = 0.0f;
+    if (!nf && thr >= 0.0 && n > 0) {
+        const float rx = v[2] - v[0], ry = v[3] - v[1];
+        const float mx = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[2])), 1e-30f);
+        const float my = fmaxf(fmaxf(fabsf(v[1]), fabsf(v[3])), 1e-30f);
+        const float minc_x = mx * 0x1p-16f, minc_y = my * 0x1p-16f;
+        h.gx = rx > 0.0f ? (int)fminf((float)GB, fmaxf(1.0f, floorf(rx / minc_x))) : 1;
+        h.gy = ry > 0.0f ? (int)fminf((float)GB, fmaxf(1.0f, floorf(ry / minc_y))) : 1;
+        h.icx = rx > 0.0f ? (float)h.gx / rx : 0.0f;
+        h.icy = ry > 0.0f ? (float)h.gy / ry : 0.0f;
+    }
+    w.hdr[g] = h;
+}
+
+__device__ __forceinline__ int cell_of(float v, float v0, float ic, int gn) {
+    const float c = floorf((v - v0) * ic);
+    return c < 0.0f ? 0 : c >= (float)(gn - 1) ? gn - 1 : (int)c;  // (NaN: gn - 1)
+}
+
+// per sorted box: its cell; counting pass (MODE 0) or the fill (MODE 1)
+template <int MODE>
+__global__ void bin_kernel(const int64_t *__restrict__ cand_off, NmsWork w) {
+    const int g = blockIdx.y;
+    const int64_t off = cand_off[g];
+    const int n = (int)(cand_off[g + 1] - off);
+    const BinHdr h = w.hdr[g];
+    int32_t *cnt = w.cnt + (size_t)g * NCELL;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const float4 bb = reinterpret_cast<const float4 *>(w.sb)[off + p];
+        const int c = cell_of(bb.y, h.y0, h.icy, h.gy) * h.gx + cell_of(bb.x, h.x0, h.icx, h.gx);
+        if (MODE == 0) {
+            atomicAdd(cnt + c, 1);
+        } else {
+            const int e = w.cst[(size_t)g * (NCELL + 1) + c] + atomicAdd(cnt + c, 1);
+            w.clist[off + e] = p;
+            reinterpret_cast<float4 *>(w.cbox)[off + e] = bb;
+        }
     }
 }
 
-// One block of RT threads per image.  Every wave resolves the block's greedy
-// chain itself (the same 64 diagonal words and the same removed word, so the
-// same kept mask, with no barrier to broadcast it); wave 0 writes the kept
-// rows; the OR of the kept rows' words into the later column blocks -- the
-// bulk of the work, (nb - ib) words per kept row -- is spread over all RT
-// threads (one wave per image left 8 waves running chip-wide at config E).
-constexpr int RT = 256;
+// exclusive scan of the cell counts per image (one block per image); the
+// counts are reset to 0 for the fill's cursors
+__global__ __launch_bounds__(256) void bin_scan_kernel(NmsWork w) {
+    __shared__ int part[256];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    int32_t *cnt = w.cnt + (size_t)g * NCELL;
+    int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
+    constexpr int PER = NCELL / 256;
+    int loc[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        loc[k] = cnt[tid * PER + k];
+        sum += loc[k];
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int t = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += t;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        cst[tid * PER + k] = run;
+        run += loc[k];
+        cnt[tid * PER + k] = 0;
+    }
+    if (tid == 255) cst[NCELL] = part[255];
+}
 
-__global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restrict__ cand_off,
-                                                          const int64_t *__restrict__ nb_off, int64_t S,
-                                                          int64_t s, NmsWork w, float *__restrict__ out_logits,
-                                                          float *__restrict__ out_boxes,
-                                                          float *__restrict__ out_refs,
-                                                          int64_t *__restrict__ out_keep,
-                                                          int32_t *__restrict__ kept_out) {
-    extern __shared__ uint64_t removed[];
-    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const bool w0 = tid < 64;
+// the cells a box's partners can lie in: corner windows
+// x1_j in (x1_i - wmax, x2_i), y1_j in (y1_i - hmax, y2_i), one cell of slack
+__device__ __forceinline__ void window(const BinHdr &h, float4 bi, int &ax0, int &ax1, int &ay0, int &ay1) {
+    if (h.gx == 1 && h.gy == 1) {
+        ax0 = ax1 = ay0 = ay1 = 0;
+        return;
+    }
+    ax0 = max(cell_of(bi.x - h.wmax, h.x0, h.icx, h.gx) - 1, 0);
+    ax1 = min(cell_of(bi.z, h.x0, h.icx, h.gx) + 1, h.gx - 1);
+    ay0 = max(cell_of(bi.y - h.hmax, h.y0, h.icy, h.gy) - 1, 0);
+    ay1 = min(cell_of(bi.w, h.y0, h.icy, h.gy) + 1, h.gy - 1);
+    if (!(bi.z >= bi.x)) ax1 = h.gx - 1;  // inverted / NaN extents: the whole row of cells
+    if (!(bi.w >= bi.y)) ay1 = h.gy - 1;
+}
+
+// one thread per box of image blockIdx.y, taken in cell order
+__global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ cand_off, double thr, NmsWork w) {
+    const int g = blockIdx.y;
+    const int64_t off = cand_off[g];
+    const int n = (int)(cand_off[g + 1] - off);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const BinHdr h = w.hdr[g];
+    const bool prune = thr >= 0.0;
+    const int i = w.clist[off + k];
+    const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + i];
+    const float ai = box_area(bi);
+    const int blk_end = (i | 63) + 1;  // first sorted row of the next 64-row block
+    const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
+    const int32_t *cl = w.clist + off;
+    const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
+    int32_t *lst = w.lst + (off + i) * CAP;
+    uint64_t diag = 0;
+    int cnt = 0;
+    int ax0, ax1, ay0, ay1;
+    window(h, bi, ax0, ax1, ay0, ay1);
+    for (int ay = ay0; ay <= ay1; ++ay) {
+        const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];  // the window row's cells are contiguous
+        for (int e = e0; e < e1; ++e) {
+            const int j = cl[e];
+            if (j <= i) continue;
+            const float4 bj = cb[e];
+            if (!iou_over(bi, ai, bj, box_area(bj), thr, prune)) continue;
+            if (j < blk_end) {
+                diag |= 1ull << (j & 63);
+            } else {
+                if (cnt < CAP) lst[cnt] = j;
+                ++cnt;
+            }
+        }
+    }
+    w.diag[off + i] = diag;
+    w.lcnt[off + i] = cnt;
+}
+
+// One wave per image: the greedy pass over the 64-row blocks in score order.
+__global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ cand_off, double thr, NmsWork w,
+                                                    float *__restrict__ out_logits, float *__restrict__ out_boxes,
+                                                    float *__restrict__ out_refs, int64_t *__restrict__ out_keep,
+                                                    int32_t *__restrict__ kept_out) {
+    extern __shared__ unsigned long long removed[];
+    const int g = blockIdx.x, lane = threadIdx.x;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
-    const int64_t ib0 = s * S;
-    if (ib0 >= nb) return;  // this image has no rows in the strip (block-uniform)
-    uint64_t *grem = w.removed + nb_off[g];
-    const uint64_t *mask = w.strip + S * 64 * nb_off[g];
-    for (int k = tid; k < nb; k += RT) {
-        if (s == 0) {
-            const int rem = n - k * 64;
-            removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
-        } else {
-            removed[k] = grem[k];
-        }
+    const BinHdr h = w.hdr[g];
+    const bool prune = thr >= 0.0;
+    for (int k = lane; k < nb; k += 64) {
+        const int rem = n - k * 64;
+        removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
     }
-    int cnt = s == 0 ? 0 : kept_out[g];
-    __syncthreads();
-    const int ib1 = (int)std::min<int64_t>(ib0 + S, nb);
-    // the row block's diagonal words do not depend on the chain: each is
-    // loaded one row block ahead, so its latency overlaps the previous
-    // block's OR loads instead of opening every block
-    uint64_t diag_next = (int)ib0 < ib1 && (int)ib0 * 64 + lane < n ? mask[(int64_t)lane * nb + ib0] : 0ull;
-    for (int ib = (int)ib0; ib < ib1; ++ib) {
+    const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
+    const int32_t *cl = w.clist + off;
+    const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
+    int cnt = 0;
+    // the next block's diagonal word and list count, loaded one block ahead
+    uint64_t dnext = lane < n ? w.diag[off + lane] : 0ull;
+    int lnext = lane < n ? w.lcnt[off + lane] : 0;
+    for (int ib = 0; ib < nb; ++ib) {
         const int i = ib * 64 + lane;
-        const int64_t row = (int64_t)(ib - ib0) * 64;
-        const uint64_t diag = diag_next;
-        if (ib + 1 < ib1)
-            diag_next = i + 64 < n ? mask[(row + 64 + lane) * nb + ib + 1] : 0ull;
+        const uint64_t diag = dnext;
+        const int lc = lnext;
+        if (i + 64 < n) {
+            dnext = w.diag[off + i + 64];
+            lnext = w.lcnt[off + i + 64];
+        } else {
+            dnext = 0ull;
+            lnext = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint64_t word = removed[ib];
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
-        // walk the surviving rows only (lowest first): each kept row's
-        // diagonal word suppresses later rows of the block
-        for (uint64_t avail = ~word; avail;) {
+        for (uint64_t avail = ~word; avail;) {  // the surviving rows, lowest first
             const int bit = __builtin_ctzll(avail);
             kept |= 1ull << bit;
             const uint32_t lo = __builtin_amdgcn_readlane(dlo, bit);
@@ -255,7 +383,8 @@ __global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restr
             word |= ((uint64_t)hi << 32) | lo;
             avail = bit == 63 ? 0ull : ~word & (~0ull << (bit + 1));
         }
-        if (w0 && ((kept >> lane) & 1ull)) {
+        const bool mine = (kept >> lane) & 1ull;
+        if (mine) {
             const int pos = cnt + __popcll(kept & ((1ull << lane) - 1));
             const int li = min(max(w.order[off + i], 0), n - 1);
             const int64_t src = off + li, dst = off + pos;
@@ -267,32 +396,34 @@ __global__ __launch_bounds__(RT) void reduce_strip_kernel(const int64_t *__restr
             if (out_keep) out_keep[dst] = li;
         }
         cnt += __popcll(kept);
-        // OR the kept rows' words into the later blocks: thread t gathers
-        // column block ib+1+t (coalesced across lanes); the kept rows (a
-        // block-uniform set) are walked 8 at a time so 8 independent loads
-        // are in flight per wait instead of one load latency per kept row
-        for (int k = ib + 1 + tid; k < nb; k += RT) {
-            uint64_t acc = 0;
-            uint64_t kb = kept;
-            while (kb) {
-                uint64_t v[8];
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    v[t] = 0;
-                    if (kb) {
-                        const int b = __builtin_ctzll(kb);
-                        kb &= kb - 1;
-                        v[t] = mask[(row + b) * nb + k];
-                    }
-                }
-                acc |= ((v[0] | v[1]) | (v[2] | v[3])) | ((v[4] | v[5]) | (v[6] | v[7]));
-            }
-            removed[k] |= acc;
+        // the kept rows' later-block suppressions into the bitmap
+        const int m = mine ? min(lc, CAP) : 0;
+        const int32_t *li_ = w.lst + (off + i) * CAP;
+        for (int e = 0; e < m; ++e) {
+            const int j = li_[e];
+            atomicOr(&removed[j >> 6], 1ull << (j & 63));
         }
-        __syncthreads();
+        // a kept row with more than CAP: the wave rescans its window
+        for (uint64_t ovf = __ballot(mine && lc > CAP); ovf; ovf &= ovf - 1) {
+            const int r = __builtin_ctzll(ovf);
+            const int ir = ib * 64 + r;
+            const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + ir];
+            const float ai = box_area(bi);
+            int ax0, ax1, ay0, ay1;
+            window(h, bi, ax0, ax1, ay0, ay1);
+            for (int ay = ay0; ay <= ay1; ++ay) {
+                const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];
+                for (int e = e0 + lane; e < e1; e += 64) {
+                    const int j = cl[e];
+                    if (j < (ib + 1) * 64) continue;
+                    if (iou_over(bi, ai, cb[e], box_area(cb[e]), thr, prune))
+                        atomicOr(&removed[j >> 6], 1ull << (j & 63));
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    for (int k = tid; k < nb; k += RT) grem[k] = removed[k];
-    if (tid == 0) kept_out[g] = cnt;
+    if (lane == 0) kept_out[g] = cnt;
 }
 
 // Calls whose every image has at most SMALL_N candidates (the module API's
@@ -451,9 +582,7 @@ __global__ __launch_bounds__(SMALL_N) void nms_small_dev_kernel(
 
 extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
     if (total_cand < 0 || sum_nb < 0 || max_cand < 0 || G <= 0) return -1;
-    int64_t S, words;
-    strip_plan(sum_nb, (max_cand + 63) / 64, S, words);
-    return work_bytes(total_cand, sum_nb, words, G);
+    return work_bytes(total_cand, G);
 }
 
 extern "C" int tmr_nms_small(const float *logits, const float *box, const float *ref, const int32_t *counts,
@@ -489,9 +618,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
         TMR_CHECK_LAUNCH();
         return TMR_OK;
     }
-    int64_t S, strip_words;
-    strip_plan(sum_nb, max_nb, S, strip_words);
-    NmsWork w = carve(work, total_cand, sum_nb, strip_words, G);
+    NmsWork w = carve(work, total_cand, G);
     hipLaunchKernelGGL(gather_kernel, dim3(G), dim3(256), 0, s, logits, box, ref, counts, unit_off,
                        seg_units, cand_off, w);
     TMR_CHECK_LAUNCH();
@@ -505,22 +632,25 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
                                                  (unsigned)total_cand, (unsigned)G, cand_off, cand_off + 1,
                                                  0, 32, s) != hipSuccess)
         return TMR_E_HIP;
-    const size_t lds = sizeof(uint64_t) * (size_t)max_nb;
-    auto rk = reduce_strip_kernel;
-    if (lds > 64 * 1024 &&
-        tmr_set_max_lds((const void *)rk, lds) !=
-            hipSuccess)
-        return TMR_E_HIP;
-    hipLaunchKernelGGL(sort_boxes_kernel, dim3((unsigned)std::min<int64_t>(tmr_cdiv(max_cand, 256), 1024), G),
-                       dim3(256), 0, s, cand_off, G, w);
+    const dim3 per_box((unsigned)std::min<int64_t>(tmr_cdiv(max_cand, 256), 1024), G);
+    hipLaunchKernelGGL(sort_boxes_kernel, per_box, dim3(256), 0, s, cand_off, G, w);
     TMR_CHECK_LAUNCH();
-    for (int64_t st = 0; st * S < max_nb; ++st) {
-        hipLaunchKernelGGL(mask_strip_kernel, dim3((unsigned)tmr_cdiv(max_nb, NJ), (unsigned)S, G), dim3(64 * MW), 0, s,
-                           cand_off, nb_off, iou_threshold, S, st, w);
-        TMR_CHECK_LAUNCH();
-        hipLaunchKernelGGL(rk, dim3(G), dim3(RT), lds, s, cand_off, nb_off, S, st, w, out_logits, out_boxes,
-                           out_refs, out_keep, kept);
-        TMR_CHECK_LAUNCH();
-    }
+    hipLaunchKernelGGL(bin_setup_kernel, dim3(G), dim3(256), 0, s, cand_off, iou_threshold, w);
+    TMR_CHECK_LAUNCH();
+    if (hipMemsetAsync(w.cnt, 0, sizeof(int32_t) * NCELL * (size_t)G, s) != hipSuccess) return TMR_E_HIP;
+    hipLaunchKernelGGL(bin_kernel<0>, per_box, dim3(256), 0, s, cand_off, w);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bin_scan_kernel, dim3(G), dim3(256), 0, s, w);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bin_kernel<1>, per_box, dim3(256), 0, s, cand_off, w);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(pairs_kernel, dim3((unsigned)tmr_cdiv(max_cand, 256), G), dim3(256), 0, s, cand_off,
+                       iou_threshold, w);
+    TMR_CHECK_LAUNCH();
+    const size_t lds = sizeof(uint64_t) * (size_t)max_nb;
+    if (lds > 64 * 1024 && tmr_set_max_lds((const void *)greedy_kernel, lds) != hipSuccess) return TMR_E_HIP;
+    hipLaunchKernelGGL(greedy_kernel, dim3(G), dim3(64), lds, s, cand_off, iou_threshold, w, out_logits,
+                       out_boxes, out_refs, out_keep, kept);
+    TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

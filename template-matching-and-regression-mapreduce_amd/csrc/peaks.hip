@@ -2,13 +2,12 @@
 // (utils/TM_utils.py:245-282) with adaptive_kernel_generater's 3x3 mask
 // (:363-377) and custom_shape_3x3_maxpool2d (:337-361, zero padding).
 //
-//   1. prob_kernel:  p = sigmoid(o) (near-correctly rounded) or p = o.
-//   2. peaks_kernel: one 1024-thread workgroup per unit; each lane owns a
-//      contiguous run of pixels, flags p >= thr && p == masked 3x3 max,
-//      a workgroup prefix sum gives each candidate its row-major slot
-//      (torch.where order, no cap), and the candidate is decoded in place:
-//      ref = (x/W, y/H); xy = ref + r[:2]*s; wh = exp(r[2:])*(bw,bh);
-//      box = (xy - wh/2, xy + wh/2).
+//   peaks_kernel: one workgroup per unit, one pass: p = sigmoid(o)
+//   (near-correctly rounded; or p = o) staged in LDS by row chunks, flags
+//   p >= thr && p == masked 3x3 max, wave ballots + mbcnt + a workgroup scan
+//   give each candidate its row-major slot (torch.where order, no cap), and
+//   the candidate is decoded in place: ref = (x/W, y/H); xy = ref + r[:2]*s;
+//   wh = exp(r[2:])*(bw,bh); box = (xy - wh/2, xy + wh/2).
 // exp: the reference's torch.exp (ATen CPU -> MKL VML vsExp, high accuracy)
 // restated as the correctly rounded value except at the inputs recorded in
 // the reference-exp table (tmr_amd/exp_table.py), where MKL rounds to the
@@ -19,7 +18,6 @@
 
 namespace {
 
-constexpr int NT = 1024;
 constexpr int EXP_HEADER = 128;  // tmr_amd/exp_table.py
 
 struct ExpTable {
@@ -42,14 +40,6 @@ __device__ __forceinline__ float expf_ref(float x, ExpTable t) {
     if (s < end && t.lo[s] == key)  // MKL rounded to the exact value's other side
         y = e > (double)y ? nextafterf(y, __builtin_inff()) : nextafterf(y, -__builtin_inff());
     return y;
-}
-
-__global__ void prob_kernel(const float *__restrict__ o, int64_t n, int is_prob,
-                            float *__restrict__ p) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float v = o[i];
-    p[i] = is_prob ? v : tmr_sigmoid_cr(v);
 }
 
 // custom_shape_3x3_maxpool2d (TM_utils.py:337-361): per element, the max of
@@ -77,89 +67,112 @@ __global__ void maxpool3x3_kernel(const float *__restrict__ x, int64_t n, int H,
     out[i] = mx;
 }
 
-__device__ __forceinline__ bool is_peak(const float *__restrict__ p, int H, int W, int y, int x,
-                                        int mask, float thr) {
-    const float v = p[y * W + x];
-    if (!(v >= thr)) return false;
-    float mx = 0.0f;
-    bool first = true;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (!((mask >> ((dy + 1) * 3 + dx + 1)) & 1)) continue;
-            const int yy = y + dy, xx = x + dx;
-            const float q = (yy < 0 || yy >= H || xx < 0 || xx >= W) ? 0.0f : p[yy * W + xx];
-            if (first || q > mx) { mx = q; first = false; }
-        }
-    return mx == v;
-}
+// One workgroup per unit, one pass (north_star kernel 4, "wavefront-ballot"):
+// the unit's map is walked in chunks of R whole rows; each chunk and its two
+// halo rows (zero outside the image: F.unfold's padding) are staged in LDS as
+// probabilities (sigmoid computed once per staged element, the chunk's own
+// rows also written to `prob`).  Then every wave takes 64 consecutive
+// row-major pixels per step: is_peak from LDS, a 64-bit ballot, mbcnt for the
+// lane's in-order slot, and a workgroup scan of the waves' popcounts for the
+// wave's base -- so the candidates leave in row-major (torch.where) order in
+// ONE pass, decoded in place.  Round 4's kernel gave each thread a contiguous
+// run of pixels (lanes strided by that run: uncoalesced loads) and evaluated
+// the 9-tap test twice (count pass, write pass).
+constexpr int PNT = 512;                // threads per unit block
+constexpr int PNW = PNT / 64;           // waves
+constexpr int PCHUNK = 2048;            // staged pixels per chunk (whole rows)
 
-__global__ __launch_bounds__(NT) void peaks_kernel(const float *__restrict__ prob,
-                                                   const float *__restrict__ reg, int H, int W,
-                                                   const tmr_peak_param_t *__restrict__ params,
-                                                   float *__restrict__ logits, float *__restrict__ box,
-                                                   float *__restrict__ ref, int32_t *__restrict__ counts,
-                                                   ExpTable et) {
-    __shared__ int wsum[NT / 64];
-    const int u = blockIdx.x;
+__host__ __device__ inline int peak_rows(int W) { return W >= PCHUNK ? 1 : PCHUNK / W; }
+
+__global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o, int is_prob,
+                                                    const float *__restrict__ reg, int H, int W,
+                                                    const tmr_peak_param_t *__restrict__ params,
+                                                    float *__restrict__ prob, float *__restrict__ logits,
+                                                    float *__restrict__ box, float *__restrict__ ref,
+                                                    int32_t *__restrict__ counts, ExpTable et) {
+    extern __shared__ float sp[];  // [R + 2][W] probabilities, row 0 = image row r0 - 1
+    __shared__ int wcnt[PNW];
+    const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const tmr_peak_param_t pp = params[u];
-    const int HW = H * W;
-    const float *p = prob + (size_t)u * HW;
-    const int per = (HW + NT - 1) / NT;
-    const int beg = min(threadIdx.x * per, HW), end = min(beg + per, HW);
-    // pass 1: count (bits of up to 64 owned pixels kept in a register mask)
-    int cnt = 0;
-    for (int i = beg; i < end; ++i) cnt += is_peak(p, H, W, i / W, i % W, pp.mask, pp.thr);
-    // workgroup exclusive scan
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int incl = cnt;
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int wbase = 0, total = 0;
-    for (int k = 0; k < NT / 64; ++k) {
-        int s = wsum[k];
-        if (k < wave) wbase += s;
-        total += s;
-    }
-    int pos = wbase + incl - cnt;
+    const int HW = H * W, R = peak_rows(W);
+    const float *ou = o + (size_t)u * HW;
+    float *pu = prob + (size_t)u * HW;
+    const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
     const size_t cap = (size_t)HW;
-    if (threadIdx.x == 0) {
-        counts[u] = total;
-        if (total == 0) {  // the empty unit's dummy row (TM_utils.py:288-291) at row 0
+    const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
+    int base = 0;  // candidates so far (block-uniform)
+    for (int r0 = 0; r0 < H; r0 += R) {
+        const int rn = min(R, H - r0), np = rn * W;
+        for (int e = tid; e < (rn + 2) * W; e += PNT) {
+            const int lr = e / W, c = e - lr * W, y = r0 - 1 + lr;
+            float v = 0.0f;
+            if (y >= 0 && y < H) {
+                const float x = ou[(size_t)y * W + c];
+                v = is_prob ? x : tmr_sigmoid_cr(x);
+                if (lr >= 1 && lr <= rn) pu[(size_t)y * W + c] = v;
+            }
+            sp[e] = v;
+        }
+        __syncthreads();
+        for (int s0 = 0; s0 < np; s0 += PNT) {
+            const int i = s0 + tid;  // pixel of the chunk
+            const int ly = i / W + 1, x = i - (ly - 1) * W;
+            bool f = false;
+            float v = 0.0f;
+            if (i < np) {
+                v = sp[ly * W + x];
+                if (v >= pp.thr) {  // masked 3x3 max (TM_utils.py:337-361): first tap, then strict >
+                    float mx = 0.0f;
+                    bool first = true;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            if (!((pp.mask >> ((dy + 1) * 3 + dx + 1)) & 1)) continue;
+                            const int xx = x + dx;
+                            const float q = (xx < 0 || xx >= W) ? 0.0f : sp[(ly + dy) * W + xx];
+                            if (first || q > mx) { mx = q; first = false; }
+                        }
+                    f = mx == v;
+                }
+            }
+            const uint64_t bal = __ballot(f);
+            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+            if (lane == 0) wcnt[wave] = __popcll(bal);
+            __syncthreads();
+            int wbase = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < PNW; ++k) {
+                const int c = wcnt[k];
+                wbase += k < wave ? c : 0;
+                tot += c;
+            }
+            if (f) {
+                const int y = r0 + ly - 1, pi = y * W + x;
+                const size_t k = (size_t)u * cap + base + wbase + slot;
+                const float rx = (float)x / (float)W, ry = (float)y / (float)H;
+                float r0v = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+                if (pp.mode != 2 && r) {
+                    r0v = r[pi]; r1 = r[HW + pi]; r2 = r[2 * HW + pi]; r3 = r[3 * HW + pi];
+                }
+                const float cx = rx + r0v * sx, cy = ry + r1 * sy;
+                const float w = expf_ref(r2, et) * pp.scale_w, h = expf_ref(r3, et) * pp.scale_h;
+                const float hw2 = w / 2.0f, hh2 = h / 2.0f;
+                *reinterpret_cast<float2 *>(logits + 2 * k) = float2{v, 0.0f};
+                *reinterpret_cast<float4 *>(box + 4 * k) = float4{cx - hw2, cy - hh2, cx + hw2, cy + hh2};
+                *reinterpret_cast<float2 *>(ref + 2 * k) = float2{rx, ry};
+            }
+            base += tot;
+            __syncthreads();  // wcnt (and, after the last step, sp) free again
+        }
+    }
+    if (tid == 0) {
+        counts[u] = base;
+        if (base == 0) {  // the empty unit's dummy row (TM_utils.py:288-291) at row 0
             *reinterpret_cast<float2 *>(logits + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
             *reinterpret_cast<float4 *>(box + (size_t)u * cap * 4) = float4{0.0f, 0.0f, 1e-14f, 1e-14f};
             *reinterpret_cast<float2 *>(ref + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
         }
-    }
-    if (cnt == 0) return;
-    const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
-    for (int i = beg; i < end; ++i) {
-        const int y = i / W, x = i % W;
-        if (!is_peak(p, H, W, y, x, pp.mask, pp.thr)) continue;
-        const size_t k = (size_t)u * cap + pos++;
-        const float v = p[i];
-        const float rx = (float)x / (float)W, ry = (float)y / (float)H;
-        float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
-        if (pp.mode != 2 && r) {
-            r0 = r[i]; r1 = r[HW + i]; r2 = r[2 * HW + i]; r3 = r[3 * HW + i];
-        }
-        const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
-        const float cx = rx + r0 * sx, cy = ry + r1 * sy;
-        const float w = expf_ref(r2, et) * pp.scale_w, h = expf_ref(r3, et) * pp.scale_h;
-        const float hw2 = w / 2.0f, hh2 = h / 2.0f;
-        logits[2 * k + 0] = v;
-        logits[2 * k + 1] = 0.0f;
-        box[4 * k + 0] = cx - hw2;
-        box[4 * k + 1] = cy - hh2;
-        box[4 * k + 2] = cx + hw2;
-        box[4 * k + 3] = cy + hh2;
-        ref[2 * k + 0] = rx;
-        ref[2 * k + 1] = ry;
     }
 }
 
@@ -189,12 +202,11 @@ extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *
         et.off = reinterpret_cast<const uint32_t *>(base + EXP_HEADER);
         et.lo = reinterpret_cast<const uint16_t *>(base + EXP_HEADER + 4 * 65537);
     }
-    int64_t n = (int64_t)U * H * W;
-    hipLaunchKernelGGL(prob_kernel, dim3((unsigned)tmr_cdiv(n, 256)), dim3(256), 0, s, o, n,
-                       input_is_prob, prob);
-    TMR_CHECK_LAUNCH();
-    hipLaunchKernelGGL(peaks_kernel, dim3(U), dim3(NT), 0, s, prob, reg, H, W, params, logits, box, ref,
-                       counts, et);
+    TMR_REQUIRE(W <= 16384);
+    const size_t lds = (size_t)(peak_rows(W) + 2) * W * sizeof(float);
+    if (lds > 64 * 1024 && tmr_set_max_lds((const void *)peaks_kernel, lds) != hipSuccess) return TMR_E_HIP;
+    hipLaunchKernelGGL(peaks_kernel, dim3(U), dim3(PNT), lds, s, o, input_is_prob, reg, H, W, params, prob,
+                       logits, box, ref, counts, et);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

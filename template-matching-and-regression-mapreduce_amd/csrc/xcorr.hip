@@ -46,10 +46,34 @@ struct XArgs {
     float *out;
     float *relu_out;
     float *work;
-    unsigned *out_absmax;  // nullable [TMR_ABSMAX_SLOTS]: slot-wise atomicMax of |out|
+    unsigned *out_absmax;  // nullable [U]: per-unit atomicMax of |out| (unit_max_*)
     int C, H, W, RB, squeeze, LR;  // LR = LDS rows allocated
     int HG;                          // rows kernel: max template height / 2
 };
+
+// Per-unit max |out| (the decoder's per-unit activation scale source,
+// tmr_xcorr out_absmax[u]): after each unit a wave reduces its lanes' max
+// and raises an LDS slot of the unit (UMAX slots, the image's first units;
+// later ones go straight to the global max); the block then raises each
+// used slot's global max once.  Slots are zeroed before the staging barrier.
+constexpr int UMAX = 64;
+__device__ __forceinline__ void unit_max_wave(float v, int ul, unsigned *slots, unsigned *gout) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) {
+        if (ul < UMAX)
+            atomicMax(slots + ul, __float_as_uint(v));
+        else
+            atomicMax(gout, __float_as_uint(v));
+    }
+}
+__device__ __forceinline__ void unit_max_flush(const unsigned *slots, const tmr_unit_t *units, int u_beg, int nu,
+                                               unsigned *gout) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < min(nu, UMAX); i += blockDim.x) {
+        const unsigned m = slots[i];
+        if (m) atomicMax(gout + units[u_beg + i].out_unit, m);
+    }
+}
 
 // x / d correctly rounded (= the reference's IEEE `/ (h*w + 1e-14)` in fp32)
 // from rd = RN(1/d): q = RN(x rd), then one fma residual step (Markstein).
@@ -177,13 +201,17 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
         for (int e = threadIdx.x; e < nld; e += NT) xs[e] = fc[(size_t)rlo * W + e];
     // zero the slack rows/cols the 4x4 register blocks may over-read
     for (int e = nld + threadIdx.x; e < a.LR * W + XSLACK; e += NT) xs[e] = 0.0f;
+    unsigned *slots = reinterpret_cast<unsigned *>(xs + a.LR * W + XSLACK);
+    const bool umax = a.out_absmax && !a.squeeze;
+    if (threadIdx.x < UMAX) slots[threadIdx.x] = 0u;
     __syncthreads();
 
     const size_t plane = (size_t)H * W;
-    float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
+        float vmax = 0.0f;
         const tmr_unit_t &un = a.units[u];
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane
         const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
@@ -193,9 +221,9 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
         const float sc = a.squeeze ? 1.0f : *a.scale;
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;  // correctly rounded reciprocal
-        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                              : outp + ((size_t)u * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        float *op = a.squeeze ? a.work + ((size_t)uo * a.C + c) * plane
+                              : outp + ((size_t)uo * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
         if (!a.squeeze) {  // zero border of this band ((yo, xo) stepped, no per-element division)
             int yo = yb0 + (int)threadIdx.x / W, xo = (int)threadIdx.x % W;
             const int sy = NT / W, sx = NT % W;
@@ -239,20 +267,9 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
                 }
             }
         }
+        if (umax) unit_max_wave(vmax, u - u_beg, slots, a.out_absmax + uo);
     }
-    if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
-        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-        __syncthreads();  // xs is free: every unit's reads are done
-        if ((threadIdx.x & 63) == 0) xs[threadIdx.x >> 6] = vmax;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float m = xs[0];
-            for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, xs[w]);
-            const unsigned slot = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) %
-                                  TMR_ABSMAX_SLOTS;
-            atomicMax(a.out_absmax + slot, __float_as_uint(m));
-        }
-    }
+    if (umax) unit_max_flush(slots, a.units, u_beg, u_end - u_beg, a.out_absmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -271,7 +288,7 @@ constexpr int PADR = 24;  // covers the window over-read past column W
 constexpr int TRY = 4;  // max tile rows (the LDS slack rows cover it)
 // rows kernel FMA form per template width: scalar v_fma_f32 up to this width
 // (no odd pairs to build; measured k = 3 1.79 vs 2.02 ms, k = 5 2.58 vs 2.65),
-// v_pk_fma_f32 on column pairs above it (k = 15 7.97 vs 10.81 ms; profiles/r02s_*)
+// v_pk_fma_f32 on column pairs above it (k = 15 7.97 vs 10.81 ms; profiles/archive/r02s_*)
 constexpr int XCORR_SCALAR_MAXW = 5;
 
 // (a.y, b.x) as ONE v_pk_mov_b32 (left to itself the compiler often builds
@@ -446,41 +463,34 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
         for (int k = 0; k < SU; ++k)
             if (e0 + k * NT < n4) xs4[e0 + k * NT] = v[k];
     }
+    unsigned *slots = reinterpret_cast<unsigned *>(xs + (size_t)a.LR * WS);
+    const bool umax = a.out_absmax && !a.squeeze;
+    if (threadIdx.x < UMAX) slots[threadIdx.x] = 0u;
     __syncthreads();
 
     const size_t plane = (size_t)H * W;
-    float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
+        float vmax = 0.0f;
         const tmr_unit_t &un = units[u];  // restrict: scalar loads, no wait behind the stores
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane
         const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
         const int Ho = H - h + 1, Wo = W - w + 1;
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;  // correctly rounded reciprocal
-        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                              : outp + ((size_t)u * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        float *op = a.squeeze ? a.work + ((size_t)uo * a.C + c) * plane
+                              : outp + ((size_t)uo * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
         const float *__restrict__ tc = tmpl + toff + (size_t)c * h * w;
         // 4x4 tiles: one 16-B store per lane row (1 KB per wave row).  2x8
         // tiles (twice the FMAs per scalar tap-row load) measured 5.1 vs 5.5
         // ms at k = 9 but 10.4 vs 7.4 at k = 11 and 16.4 vs 11.4 at k = 15.
         rows_unit<4, 4, MAXW>(xs, WS, W, yb0, yb1, hg, h, w, ph, pw, Ho, Wo, tc, denom, rden, sc, op, rp, vmax);
+        if (umax) unit_max_wave(vmax, u - u_beg, slots, a.out_absmax + uo);
     }
-    if (a.out_absmax && !a.squeeze) {  // one atomic per workgroup, spread over the slots
-        for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-        __syncthreads();  // xs is free: every unit's reads are done
-        if ((threadIdx.x & 63) == 0) xs[threadIdx.x >> 6] = vmax;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float m = xs[0];
-            for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, xs[w]);
-            const unsigned slot = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) %
-                                  TMR_ABSMAX_SLOTS;
-            atomicMax(a.out_absmax + slot, __float_as_uint(m));
-        }
-    }
+    if (umax) unit_max_flush(slots, units, u_beg, u_end - u_beg, a.out_absmax);
 }
 
 
@@ -516,7 +526,7 @@ constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
 // A-fragment prefetch distance in template rows.  One-term kernel: 4 rows
 // (its rows are 1/3 the MFMA work of the 3-term kernel's, so one row ahead
 // leaves the L2 latency exposed; measured at 128^2 E = 3, config-B mix: PF
-// 1/2/3/4/5/8 = 3.74/4.10/3.61/3.09/4.56/3.24 ms, profiles/r02ad_*, r02ae_*).
+// 1/2/3/4/5/8 = 3.74/4.10/3.61/3.09/4.56/3.24 ms, profiles/archive/r02ad_*, r02ae_*).
 // 3-term kernel: 1 row (PF 2/4: 5.85/5.28 vs 4.67 ms).
 // 3-term, >= 6 tiles per wave (W >= 192, LDS-bound occupancy): 3 rows (r03t).
 constexpr int XCORR_PF1 = 4, XCORR_PF3 = 1, XCORR_PF3_WIDE = 3;
@@ -561,12 +571,14 @@ struct MArgs {
 };
 
 __device__ __forceinline__ float pow2_scale(float m, int &e) {
-    // s = 2^(14 - e') with m < 2^e' (max |x s| < 2^14); e = -log2(s)
+    // s = 2^(14 - e') with m < 2^e' (max |x s| < 2^14); e = -log2(s); s is
+    // clamped to [2^-63, 2^63] (a finite scale, whatever m is)
     if (!(m > 0.0f && m <= 3.0e38f)) { e = 0; return 1.0f; }
     int ex;
     frexpf(m, &ex);
-    e = ex - 14;
-    return ldexpf(1.0f, 14 - ex);
+    const int se = min(max(14 - ex, -63), 63);
+    e = -se;
+    return ldexpf(1.0f, se);
 }
 
 __device__ __forceinline__ float block_max(float v, float *red) {
@@ -585,7 +597,7 @@ __device__ __forceinline__ float block_max(float v, float *red) {
 // T[i][8g + 32nk + q - m - s], q = 0..7 (zero outside [0, w)).  The kernel's
 // A load is then one aligned, contiguous 1-KB wave read.  (Loading the same
 // 16-B windows at 2-B-aligned offsets out of padded template rows -- round 2's
-// first layout -- cost 17-21% of the kernel at k = 15: profiles/r02u_*.)
+// first layout -- cost 17-21% of the kernel at k = 15: profiles/archive/r02u_*.)
 // One wave per (unit, channel).
 constexpr int AFRAG = 64 * 16;  // bytes per (row, nk, term) fragment
 
@@ -664,7 +676,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 if (lo_too) *reinterpret_cast<h8 *>(f + AFRAG) = lo;  // the 3-term kernel's tl
             }
         }
-    if (lane == 0) exps[(int64_t)u * C + c] = et;
+    if (lane == 0) exps[(int64_t)un.out_unit * C + c] = et;  // (the unit's row in the full set)
 }
 
 // one unit over the band: acc[t] += sum_i A_i B_i over the wave's NTW tiles
@@ -673,7 +685,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
 // pre-expanded fragments (tmr_template_split; arow = this lane's slot of
 // row 0), issued PF template rows ahead of their MFMAs.  (Measured: staging
 // them through an LDS table per row chunk, with its two barriers per chunk,
-// was slower at every k >= 11; profiles/r02b_kbench_xcorr_*.)
+// was slower at every k >= 11; profiles/archive/r02b_kbench_xcorr_*.)
 template <int NTW, int NK, int WPR, int PM>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
                                           int h, const char *arow, int tcol0, int pw_al, int g) {
@@ -757,12 +769,22 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     if (u_beg >= u_end) return;
     char *Fh = smem, *Fl = smem + (size_t)LR * SB;  // Fl: F16X3 only
     float *red = reinterpret_cast<float *>(smem + NPL * (size_t)LR * SB);
+    unsigned *slots = reinterpret_cast<unsigned *>(red + 16);  // [UMAX] per-unit max |out|
     const int tid = threadIdx.x;
+    const bool umax = a.out_absmax && !a.squeeze;
+    if (tid < UMAX) slots[tid] = 0u;  // (ordered before the uses by block_max's barriers)
     const int yb0 = band * BR, yb1 = min(yb0 + BR, H);
     const float *__restrict__ fc = a.f + ((size_t)img * a.C + c) * H * W;
     const float sc = a.squeeze ? 1.0f : *a.scale;
 
-    // ---- stage the band: fp32 -> registers -> block max -> fp16 hi/lo planes
+    // ---- stage the band: fp32 -> registers -> block max -> fp16 hi/lo planes.
+    // Only the rows THIS image's units read (its own largest template's
+    // halo, not the launch's) are staged and enter the scale, so a unit's
+    // f_TM depends on its image and exemplars alone, never on the other
+    // images of the batch (tests/test_gpu_precision.py: batch invariance)
+    int hmax_img = 1;
+    for (int u = u_beg; u < u_end; ++u) hmax_img = max(hmax_img, __builtin_amdgcn_readfirstlane(units[u].ht));
+    const int ylo = yb0 - hmax_img / 2, yhi = yb1 + hmax_img / 2;
     const int W4 = W >> 2, n4 = LR * W4;
     const float rw4 = 1.0f / (float)W4;  // e / W4 by one multiply (exact for e < 2^16)
     float4 v[NV4];
@@ -773,7 +795,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         v[k] = float4{0.0f, 0.0f, 0.0f, 0.0f};
         const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
         const int yy = yb0 - hg + lr;
-        if (e < n4 && yy >= 0 && yy < H) v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
+        if (e < n4 && yy >= 0 && yy < H && yy >= ylo && yy < yhi)
+            v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
         vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
     }
     // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
@@ -811,12 +834,13 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     const int tcol0 = wave / TRB;    // tile cols tcol0, tcol0 + WPR, ...
     const bool row_live = yb0 + tr * 16 < yb1;
     const size_t plane = (size_t)H * W;
-    float vmax = 0.0f;
     for (int u = u_beg; u < u_end; ++u) {
+        float vmax = 0.0f;
         const tmr_unit_t &un = units[u];
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
+        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane (texp row)
         const int roff = __builtin_amdgcn_readfirstlane(un.row_offset);
-        const int et = __builtin_amdgcn_readfirstlane(texp[(size_t)u * a.C + c]);
+        const int et = __builtin_amdgcn_readfirstlane(texp[(size_t)uo * a.C + c]);
         const int ph = h / 2, pw = w / 2, Ho = H - h + 1, Wo = W - w + 1;
         const int pw_al = (pw + 7) & ~7, s = pw_al - pw;
         f32x4 acc[NTW];
@@ -835,10 +859,10 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
         const float denom = (float)(h * w);
         const float rden = 1.0f / denom;
-        float *op = a.squeeze ? a.work + ((size_t)u * a.C + c) * plane
-                    : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)u * a.C + c) * plane)
-                         : outp + ((size_t)u * a.C + c) * plane;
-        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)u * a.C + c) * plane : nullptr;
+        float *op = a.squeeze ? a.work + ((size_t)uo * a.C + c) * plane
+                    : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)uo * a.C + c) * plane)
+                         : outp + ((size_t)uo * a.C + c) * plane;
+        float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
         const int y = yb0 + tr * 16 + l16;
         if (row_live && y < yb1) {
             const bool vy = y >= ph && y < ph + Ho;
@@ -863,11 +887,9 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                         float4{fmaxf(r4[0], 0.0f), fmaxf(r4[1], 0.0f), fmaxf(r4[2], 0.0f), fmaxf(r4[3], 0.0f)};
             }
         }
+        if (umax) unit_max_wave(vmax, u - u_beg, slots, a.out_absmax + uo);
     }
-    if (a.out_absmax && !a.squeeze) {
-        const float mx = block_max(vmax, red);
-        if (tid == 0) atomicMax(a.out_absmax + (unsigned)q % TMR_ABSMAX_SLOTS, __float_as_uint(mx));
-    }
+    if (umax) unit_max_flush(slots, units, u_beg, u_end - u_beg, a.out_absmax);
 }
 
 // smallest LDS row stride >= bytes with stride = 32 mod 64 (conflict-free B reads)
@@ -899,12 +921,22 @@ __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_u
         out[i] = v;
         if (relu_out) relu_out[i] = v > 0.0f ? v : 0.0f;
     }
-    if (out_absmax) {
-        float m = fabsf(v);
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        if ((threadIdx.x & 63) == 0)
-            atomicMax(out_absmax + (blockIdx.x * 4 + (threadIdx.x >> 6)) % TMR_ABSMAX_SLOTS,
-                      __float_as_uint(m));
+    if (out_absmax) {  // per unit: a wave covers at most two units when H*W >= 64
+        const int64_t tot = (int64_t)U * H * W;
+        const int u = i < tot ? (int)(i / ((int64_t)H * W)) : -1;
+        const int u0 = __builtin_amdgcn_readfirstlane(u);
+        float m0 = u == u0 ? fabsf(v) : 0.0f, m1 = u != u0 ? fabsf(v) : 0.0f;
+        for (int o = 32; o > 0; o >>= 1) {
+            m0 = fmaxf(m0, __shfl_xor(m0, o));
+            m1 = fmaxf(m1, __shfl_xor(m1, o));
+        }
+        const int u1 = __shfl(u, 63);
+        if ((threadIdx.x & 63) == 0 && u0 >= 0) atomicMax(out_absmax + u0, __float_as_uint(m0));
+        if ((int64_t)H * W >= 64) {
+            if ((threadIdx.x & 63) == 0 && u1 >= 0 && u1 != u0) atomicMax(out_absmax + u1, __float_as_uint(m1));
+        } else if (u >= 0 && u != u0) {
+            atomicMax(out_absmax + u, __float_as_uint(fabsf(v)));
+        }
     }
 }
 
@@ -954,7 +986,7 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
                        const void *tmpl_split, int64_t total_rows, int prec, bool out16) {
     MArgs m;
     // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
-    // 1.7-1.9x slower at k >= 17, profiles/r02b_kbench_xcorr_*)
+    // 1.7-1.9x slower at k >= 17, profiles/archive/r02b_kbench_xcorr_*)
     const int trb = 2;
     m.HG = max_ht / 2;
     m.HTM = max_ht;
@@ -965,7 +997,7 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
     const int64_t nlog = (int64_t)m.nband * a.C * B;
     TMR_REQUIRE(nlog < (1LL << 31) - 8);
     m.nlog = (int)nlog;
-    const size_t lds = (prec == TMR_PREC_F16X3 ? 2 : 1) * (size_t)m.LR * m.SB + 64;
+    const size_t lds = (prec == TMR_PREC_F16X3 ? 2 : 1) * (size_t)m.LR * m.SB + 64 + 4 * UMAX;
     const unsigned nblk = (unsigned)((nlog + 7) / 8 * 8);
     const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
     const int32_t *texp = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
@@ -1054,8 +1086,8 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
         a.RB = RB;
         a.LR = rows ? RB + max_ht + 3 : RB + max_ht - 1 + RY;
         a.HG = max_ht / 2;
-        const size_t lds = rows ? (size_t)a.LR * WS * sizeof(float)
-                                : ((size_t)a.LR * W + XSLACK) * sizeof(float);
+        const size_t lds = (rows ? (size_t)a.LR * WS * sizeof(float)
+                                 : ((size_t)a.LR * W + XSLACK) * sizeof(float)) + 4 * UMAX;
         const bool narrow = max_wt <= 15;
         const void *kfn = !rows ? (const void *)xcorr_kernel
                           : narrow ? (const void *)xcorr_rows_kernel<15> : (const void *)xcorr_rows_kernel<31>;

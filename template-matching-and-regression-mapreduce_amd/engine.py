@@ -32,11 +32,10 @@ import torch
 
 from . import exp_table, host
 from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
-                   SPLIT_TILED_OUT, UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr, require_gpu,
-                   stream)
+                   SPLIT_TILED_OUT, SPLIT_XMAX_PER_PIXEL, SPLIT_XMAX_PER_UNIT, UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr,
+                   require_gpu, stream)
 
 NHEAD = 5
-ABSMAX_SLOTS = 256  # TMR_ABSMAX_SLOTS (include/tmr.h)
 NMS_SMALL = 256  # TMR_NMS_SMALL (include/tmr.h)
 
 
@@ -72,7 +71,7 @@ class PathConfig:
 # durations of both kernels per k in the two regimes, beside each point's
 # counted HBM bytes and MFMA busy (profiles/xcorr_crossover.json; DESIGN.md
 # 4.3).  The constants here are the round-2 HIP-event tables it replaced
-# (kbench_xcorr, profiles/r02w_sweep{128,192}.jsonl), as ms per unit at the
+# (kbench_xcorr, profiles/archive/r02w_sweep{128,192}.jsonl), as ms per unit at the
 # 512 x 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
 # exemplars at 128^2; the image's band staging is shared by 3 units) and
 # E = 16 (8 images x 16 exemplars at 192^2, times / 2.25 for the area).
@@ -81,7 +80,7 @@ class PathConfig:
 # VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
 # crossover); at E = 16 MFMA wins from k = 9 on.  Under the bf16 contract
 # (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr_prec) the MFMA
-# kernel wins from k = 5 at E = 3 (profiles/r02af_*).
+# kernel wins from k = 5 at E = 3 (profiles/archive/r02af_*).
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
 _T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
     "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
@@ -100,7 +99,7 @@ XCORR_COST = {
         np.interp(XCORR_COST_K, _K192, np.asarray(_T192[a]) / 128.0 / 2.25))
     for a in ("valu", "mfma", "mfma1")
 }
-XCORR_COST_SOURCE = "engine.py tables (HIP events, profiles/r02w_*, r02af_*)"
+XCORR_COST_SOURCE = "engine.py tables (HIP events, profiles/archive/r02w_*, r02af_*)"
 # The committed rocprofv3 sweep (profiles/gpu_xcorr_sweep.sh ->
 # profiles/xcorr_sweep_assemble.py -> xcorr_cost.json: kernel-trace launch
 # durations of both kernels per k and regime, recorded beside their FETCH /
@@ -146,9 +145,9 @@ if _swept is not None:
 # rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
 # units when an image has few of them: measured 1.13x the per-k sum at the
 # config-B 3..15 mix with 3 units per image (5.57 ms vs 4.91,
-# profiles/r02b_kbench_xcorr_mixB*; 1.10x after the aligned-fragment change,
-# 4.75 vs 4.30, profiles/r02w_mixB.jsonl), 1.46x for the k >= 11 units of that
-# batch (~2 per image; profiles/r02c_bench_B* by_class); the VALU kernel's
+# profiles/archive/r02b_kbench_xcorr_mixB*; 1.10x after the aligned-fragment change,
+# 4.75 vs 4.30, profiles/archive/r02w_mixB.jsonl), 1.46x for the k >= 11 units of that
+# batch (~2 per image; profiles/archive/r02c_bench_B* by_class); the VALU kernel's
 # mixes run 1.00-1.04x its per-k sums.  Empirical: 1 + 0.4 / units-per-image.
 XCORR_MFMA_MIX = 0.4
 
@@ -170,6 +169,19 @@ def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok
     if k.size and k.min() != k.max():
         cost["mfma"] *= 1.0 + XCORR_MFMA_MIX / max(units_per_image, 1.0)
     return min(cost, key=cost.get)
+
+
+def xcorr_unit_split(ht: np.ndarray, wt: np.ndarray, units_per_image: float, one_term: bool = False):
+    """Per unit, whether the MFMA correlation is the cheaper kernel for it
+    (the XCORR_COST model at this unit count per image): the unit-level
+    crossover of a launch split by kernel (TMREngine.xcorr_split)."""
+    k = np.maximum(np.asarray(ht), np.asarray(wt)).astype(np.float64)
+    lam = float(np.clip(np.log(max(units_per_image, 1.0) / 3.0) / np.log(16.0 / 3.0), 0.0, 1.0))
+    cost = {}
+    for alg, table in (("valu", "valu"), ("mfma", "mfma1" if one_term else "mfma")):
+        c3, c16 = XCORR_COST[table]
+        cost[alg] = np.interp(k, XCORR_COST_K, (1.0 - lam) * c3 + lam * c16)
+    return cost["mfma"] < cost["valu"]
 
 
 def _version_key(ts: Sequence[torch.Tensor]):
@@ -207,6 +219,62 @@ def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     return out
 
 
+def absmax_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-sample max |x[s]| of x [S, ...] as an [S] device tensor (max(out, .)
+    when out is given): the per-sample activation scale source of the split
+    kernels (tmr_absmax_rows)."""
+    require_gpu(x, "absmax input")
+    if x.dtype != torch.float32:
+        raise TMRError(f"absmax of a {x.dtype} tensor (fp32 only)")
+    x = x.contiguous()
+    S = x.shape[0]
+    acc = out is not None
+    if out is None:
+        out = torch.empty(S, device=x.device, dtype=torch.float32)
+    elif out.numel() != S:
+        raise TMRError(f"absmax_rows: out holds {out.numel()} values for {S} samples")
+    call("tmr_absmax_rows", ptr(x), S, x.numel() // max(S, 1), int(acc), ptr(out), stream())
+    return out
+
+
+def scale_merge(img_max: Optional[torch.Tensor], unit_max: torch.Tensor, unit_image: torch.Tensor, B: int):
+    """(per-image, per-unit) scale sources of a launch whose tiles read an
+    image's src0 records and its units' src1 records with ONE scale:
+    img[b] = max(img_max[b], unit_max[u] for u of image b), unit[u] =
+    img[unit_image[u]] (tmr_scale_merge)."""
+    U = unit_max.numel()
+    out_img = torch.empty(B, device=unit_max.device, dtype=torch.float32)
+    out_unit = torch.empty(U, device=unit_max.device, dtype=torch.float32)
+    call("tmr_scale_merge", ptr(img_max) if img_max is not None else None, ptr(unit_max), ptr(unit_image),
+         B, U, ptr(out_img), ptr(out_unit), stream())
+    return out_img, out_unit
+
+
+def pixel_absmax(x: torch.Tensor) -> torch.Tensor:
+    """max_c |x[s, c, y, x]| as [S, H, W] (tmr_pixel_absmax): the per-pixel
+    scale source of a 1x1 conv (TMR_SPLIT_XMAX_PER_PIXEL)."""
+    require_gpu(x, "absmax input")
+    x = x.float().contiguous()
+    S, C, H, W = x.shape
+    out = torch.empty((S, H, W), device=x.device, dtype=torch.float32)
+    call("tmr_pixel_absmax", ptr(x), S, C, H * W, ptr(out), stream())
+    return out
+
+
+def _per_sample(xmax: Optional[torch.Tensor], S: int) -> int:
+    """The xmax_per_sample mode of the record packs: 0 for one shared scale
+    source, 1 for one per sample ([S]), 2 for one per pixel ([S, H, W])."""
+    if xmax is None or xmax.numel() == 1:
+        return 0
+    if xmax.dim() == 3:
+        if xmax.shape[0] != S:
+            raise TMRError(f"per-pixel scale sources for {xmax.shape[0]} samples, not {S}")
+        return 2
+    if xmax.numel() != S:
+        raise TMRError(f"scale source holds {xmax.numel()} values for {S} samples")
+    return 1
+
+
 def prec_code(precision: str) -> int:
     if precision not in PREC_CODES:
         raise TMRError(f"precision must be one of {sorted(PREC_CODES)}, got {precision!r}")
@@ -234,7 +302,8 @@ def pack_split_w(w: torch.Tensor, c0: int, precision: str):
 def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -> torch.Tensor:
     """[S,C,H,W] fp32 -> zero-padded 16-bit records (tmr_split_xpack); a bf16
     x (the correlation's bf16 f_TM plane, tmr_xcorr_out) under the bf16
-    contract -> the same records (tmr_split_xpack16)."""
+    contract -> the same records (tmr_split_xpack16).  xmax: one scale source,
+    or [S] (one per sample)."""
     require_gpu(x, "conv input")
     S, C, H, W = x.shape
     pc = prec_code(precision)
@@ -247,7 +316,7 @@ def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -
         call("tmr_split_xpack16", ptr(x), S, C, H, W, ks, pc, ptr(out), stream())
         return out
     x = x.float().contiguous()
-    call("tmr_split_xpack", ptr(x), S, C, H, W, ks, pc, ptr(xmax), ptr(out), stream())
+    call("tmr_split_xpack", ptr(x), S, C, H, W, ks, pc, ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
     return out
 
 
@@ -280,14 +349,16 @@ def pack_split_up(f: torch.Tensor, upsample: bool, ks: int, precision: str,
         raise TMRError(f"unsupported feature shape {tuple(f.shape)}")
     out = torch.empty(n, device=f.device, dtype=torch.uint8)
     call("tmr_split_xpack_up", ptr(f), S, Cin, Hin, Win, int(upsample), int(ones), ks, pc,
-         ptr(xmax), ptr(out), stream())
+         ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
     return out
 
 
 def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
                  precision: str = "fp32", packed=None):
     """nn.Conv2d(padding=(k-1)//2) [+ LeakyReLU(0.01)] on the split 16-bit
-    MFMA kernel (precision "fp32" keeps the 1e-5 contract)."""
+    MFMA kernel (precision "fp32" keeps the 1e-5 contract).  One activation
+    scale per SAMPLE (per PIXEL for a 1x1 conv, whose output columns are
+    pixels): each sample's result is that of a batch of one."""
     require_gpu(x, "conv input")
     x = x.float().contiguous()
     U, C, H, W = x.shape
@@ -295,12 +366,13 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     if Cw != C:
         raise TMRError(f"conv expects {Cw} input channels, got {C}")
     wp, wmax = packed if packed is not None else pack_split_w(w, C, precision)
-    xmax = absmax(x)
+    pix = ks == 1
+    xmax = pixel_absmax(x) if pix else absmax_rows(x)
     xp = pack_split_x(x, ks, precision, xmax)
     out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
     call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, prec_code(precision),
          ptr(wp), ptr(wmax), ptr(xmax), ptr(b.detach().float().contiguous()), N, int(leaky), None,
-         ptr(out), 0, stream())
+         ptr(out), SPLIT_XMAX_PER_PIXEL if pix else SPLIT_XMAX_PER_UNIT, stream())
     return out
 
 
@@ -394,6 +466,56 @@ def _clone_outputs(out: Dict[str, object], keep=("fp",)) -> Dict[str, object]:
     return res
 
 
+class _GraphBook:
+    """Which launch signatures have a captured graph, how often the others
+    were seen, and which failed to capture.  A signature is
+    captured on its second sighting; the seen-counts are an LRU bounded by
+    `seen_cap` (mapper workloads with varied exemplar sizes make a new
+    signature almost every batch), graphs an LRU of `cap`, and a signature
+    whose capture failed stays eager (bounded too) instead of retrying the
+    sync + clone + capture on every call.  Host-only: tested on CPU."""
+
+    FAILED = object()
+
+    def __init__(self, cap: int, seen_cap: int = 256):
+        from collections import OrderedDict
+        self.cap, self.seen_cap = cap, seen_cap
+        self.graphs: "OrderedDict[tuple, object]" = OrderedDict()
+        self.seen: "OrderedDict[tuple, int]" = OrderedDict()
+        self.failed: "OrderedDict[tuple, None]" = OrderedDict()
+
+    def get(self, sig):
+        g = self.graphs.get(sig)
+        if g is not None:
+            self.graphs.move_to_end(sig)
+        return g
+
+    def want_capture(self, sig) -> bool:
+        """Count a sighting of sig (no graph yet); True when it should be
+        captured now (second sighting, never failed)."""
+        if sig in self.failed:
+            return False
+        n = self.seen.pop(sig, 0) + 1
+        self.seen[sig] = n
+        while len(self.seen) > self.seen_cap:
+            self.seen.popitem(last=False)
+        return n >= 2
+
+    def put(self, sig, g):
+        self.seen.pop(sig, None)
+        if g is None:
+            self.failed[sig] = None
+            while len(self.failed) > self.seen_cap:
+                self.failed.popitem(last=False)
+            return
+        self.graphs[sig] = g
+        while len(self.graphs) > self.cap:
+            self.graphs.popitem(last=False)
+
+    def clear(self):
+        self.graphs.clear(); self.seen.clear(); self.failed.clear()
+
+
 class _DetectGraph:
     """One captured detect forward (projection ... peaks) for a fixed launch
     signature: the inputs are a static feature buffer and the pinned host
@@ -405,15 +527,21 @@ class _DetectGraph:
         self.done = None  # event after the last replay: its copy node reads the pinned blob
         self.src = None  # (tensor ref, version, data_ptr) of the features last copied into feats
 
-    def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray]):
+    def replay(self, feats: torch.Tensor, host: Dict[str, np.ndarray], reuse_feats: bool = False):
+        """reuse_feats (the module API's later exemplar calls on one image,
+        where reusing the image is the intent): skip the feature copy when
+        the same tensor object at the same version was copied last.  detect()
+        always copies: writes through a raw pointer or a caller's
+        own graph replay change a tensor without bumping its version."""
         # the blob is rewritten by the host at once: a previous replay still
         # queued (two calls with no sync between them) must have read it first
         if self.done is not None:
             self.done.synchronize()
         self.blob.fill(host)
         src = self.src
-        if src is None or src[0]() is not feats or src[1] != (feats._version, feats.data_ptr()):
-            self.feats.copy_(feats)  # (the module API's later exemplars reuse the image's copy)
+        if not reuse_feats or src is None or src[0]() is not feats or \
+                src[1] != (feats._version, feats.data_ptr()):
+            self.feats.copy_(feats)
             self.src = (weakref.ref(feats), (feats._version, feats.data_ptr()))
         self.graph.replay()
         if self.done is None:
@@ -452,6 +580,11 @@ class TMREngine:
         # "valu" or "mfma" (csrc/xcorr.hip)
         self.xcorr_algo = "auto"
         self.last_xcorr_algo = None
+        # "auto" correlation of a mixed launch split by kernel per unit: the
+        # units the MFMA kernel wins on run it, the others the VALU kernel,
+        # the two launches on two streams (subset launches: tmr_unit_t.out_unit)
+        self.xcorr_split = False
+        self._side = None
         self.last_nms_small = False  # detect: the kept rows came from the in-forward small NMS
         # bf16 contract, detect path: the one-term MFMA correlation writes
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
@@ -462,8 +595,7 @@ class TMREngine:
         self.reuse_image_work = False
         self._fp_memo = None
         self._acc0_memo = None
-        self._graphs: Dict[tuple, _DetectGraph] = {}
-        self._graph_seen: Dict[tuple, int] = {}
+        self._graphs = _GraphBook(self.GRAPH_CACHE)
         self.last_graph = None
         self.last_graph_error = None
         self.last_decoder_flops = 0.0
@@ -581,13 +713,13 @@ class TMREngine:
 
     # ------------------------------------------------------------ forward
     def _feat_absmax(self, feats: torch.Tensor) -> torch.Tensor:
-        """max(1, max |feats|) as a device scalar (memoised per tensor): the
-        scale source of the [up2x(f); 1] records (bilinear weights are convex).
-        None under the bf16 contract: bf16 records and kernels are unscaled."""
+        """max |feats[b]| per image as a device [B] tensor (memoised per
+        tensor): the per-image scale source of the up2x(f) records (bilinear
+        weights are convex, so max |up2x(f)| <= max |f|).  None under the
+        bf16 contract: bf16 records and kernels are unscaled."""
         if self.cfg.precision == "bf16":
             return None
-        return self._memo_absmax(feats, "feat", lambda: absmax(
-            feats, torch.ones(1, device=feats.device, dtype=torch.float32)))
+        return self._memo_absmax(feats, "feat", lambda: absmax_rows(feats))
 
     def _memo_absmax(self, t: torch.Tensor, tag: str, compute=None):
         """Device max scalars memoised per tensor OBJECT and version (a freed
@@ -624,7 +756,11 @@ class TMREngine:
         if Cw != Cin:
             raise TMRError(f"input_proj expects {Cw} channels, got {Cin}")
         wp, wmax = self._cache.get(f"proj_split_{pprec}", [pw], lambda: pack_split_w(pw, Cin, pprec))
-        xmax = self._feat_absmax(feats)
+        # one activation scale per feature PIXEL (the max over its channels):
+        # the templates are cut from fp and renormalised per (unit, channel)
+        # by the correlation, so a quiet region of an image must keep its
+        # own fp32-grade precision (tests/test_gpu_precision.py (b))
+        xmax = None if pprec == "bf16" else pixel_absmax(feats)
         # the 1x1 projection commutes with the bilinear x2 (both linear;
         # the interpolation weights of each output sum to 1, so the bias
         # passes through): project at the features' size, then upsample
@@ -635,11 +771,11 @@ class TMREngine:
         n = load().tmr_split_xpack_size(B, Cin, Hq, Wq, 1, pcode)
         xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
         call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, 0, 0, 1, pcode,
-             ptr(xmax), ptr(xp), stream())
+             ptr(xmax), _per_sample(xmax, B), ptr(xp), stream())
         fq = torch.empty((B, N, Hq, Wq), device=feats.device, dtype=torch.float32)
         call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
              ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
-             0, stream())
+             SPLIT_XMAX_PER_PIXEL if xmax is not None else 0, stream())
         if up:
             fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
             call("tmr_upsample2x", ptr(fq), B * N, Hin, Win, ptr(fp), stream())
@@ -673,8 +809,9 @@ class TMREngine:
         Co = 1 if cfg.squeeze else C
         work = torch.empty((U, C, H, W), device=dev, dtype=torch.float32) if cfg.squeeze else None
         scale = self.P["matcher.scale"].detach().float().contiguous()
-        # max |f_TM| fused in the kernel: per-workgroup maxima into 256 slots
-        slots = torch.zeros(ABSMAX_SLOTS, device=dev, dtype=torch.float32)
+        # max |f_TM| per unit fused in the kernel (the decoder's per-unit
+        # activation scale source)
+        slots = torch.zeros(U, device=dev, dtype=torch.float32)
         ev = None
         if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -690,21 +827,34 @@ class TMREngine:
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
+        split = None
+        if self.xcorr_split and self.xcorr_algo == "auto" and fits and not cfg.squeeze and \
+                getattr(_capture, "blob", None) is None and U > 1:
+            mf = xcorr_unit_split(units["ht"], units["wt"], U / max(1, len(set(unit_image))),
+                                  one_term=pc != PREC_CODES["fp32"])
+            if mf.any() and not mf.all():
+                split = mf
+                choice = "split"
+                self.last_xcorr_algo = choice
         out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
-                 and not cfg.squeeze and not want_relu and W % 8 == 0)
+                 and not cfg.squeeze and not want_relu and W % 8 == 0 and split is None)
         self.last_xcorr_out16 = out16
         out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
         relu = torch.empty_like(out) if want_relu else None
         tsplit = None
-        if algo != XCORR_ALGOS["valu"] and tfl > 0:
-            # the MFMA correlation's template operands (per (unit, channel) scale)
-            rows = host.tsplit_rows(units)
-            tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
-            call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
-        call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
-             mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
-             ptr(work) if work is not None else None, ptr(slots), ptr(tsplit) if tsplit is not None else None,
-             rows if tsplit is not None else 0, algo, min_k, pc, int(out16), stream())
+        if split is not None:
+            self._match_split(fp, tmpl, units, unit_image, split, scale, out, relu, slots, pc)
+        else:
+            if algo != XCORR_ALGOS["valu"] and tfl > 0:
+                # the MFMA correlation's template operands (per (unit, channel) scale)
+                rows = host.tsplit_rows(units)
+                tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
+                call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
+            call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
+                 mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
+                 ptr(work) if work is not None else None, ptr(slots),
+                 ptr(tsplit) if tsplit is not None else None, rows if tsplit is not None else 0, algo, min_k, pc,
+                 int(out16), stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
@@ -718,9 +868,60 @@ class TMREngine:
         # write one f_TM plane per unit
         # (fp32 reads; the f_TM write is bf16, 2 B, under out16)
         nimg = len(set(int(i) for i in unit_image))
+        if split is not None:  # each launch stages the planes of its own units' images
+            ui_ = np.asarray(unit_image)
+            nimg = len(set(ui_[split].tolist())) + len(set(ui_[~split].tolist()))
         self.last_xcorr_dram_bytes = float(C * H * W) * (4.0 * nimg + (2.0 if out16 else 4.0) * U)
-        self._memo_absmax(out, "ftm", lambda: absmax(slots))
+        self._memo_absmax(out, "ftm", lambda: slots)
         return out, relu
+
+    def _match_split(self, fp, tmpl, units, unit_image, mfma_units, scale, out, relu, slots, pc):
+        """The correlation as two launches over complementary unit subsets
+        (each unit's output plane / max slot / exponent row = its out_unit):
+        the MFMA kernel's units on the current stream, the VALU kernel's on a
+        side stream (joined back before anything reads f_TM), so the two
+        kernels' blocks share the chip instead of one kernel running units it
+        is slower on."""
+        B, C, H, W = fp.shape
+        dev = fp.device
+        ui = np.asarray(unit_image, np.int64)
+        main = torch.cuda.current_stream(dev)
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(device=dev)
+        side = self._side
+        fork = torch.cuda.Event()
+        fork.record(main)
+        subs = []
+        for is_mfma in (False, True):
+            idx = np.nonzero(mfma_units == is_mfma)[0]
+            sub = units[idx].copy()
+            sub_ui = ui[idx]
+            subs.append((is_mfma, sub, sub_ui))
+        rows = host.tsplit_rows(units)  # absolute row offsets: the full set's buffer
+        tsplit = torch.empty(load().tmr_template_split_size(len(units), C, rows), device=dev, dtype=torch.uint8)
+        for is_mfma, sub, sub_ui in subs:
+            st = main if is_mfma else side
+            with torch.cuda.stream(st):
+                if not is_mfma:
+                    st.wait_event(fork)
+                sub_d = _units_to_device(sub, dev)
+                iu_d = _h2d(host.image_ranges(sub_ui, B), dev)
+                mh, mw = int(sub["ht"].max()), int(sub["wt"].max())
+                min_k = int(min(sub["ht"].min(), sub["wt"].min()))
+                if is_mfma:
+                    call("tmr_template_split_prec", ptr(tmpl), ptr(sub_d), len(sub), C, rows, pc, ptr(tsplit),
+                         stream())
+                call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(sub_d), ptr(iu_d), len(sub), mh, mw,
+                     ptr(scale), 0, ptr(out), ptr(relu) if relu is not None else None, None, ptr(slots),
+                     ptr(tsplit) if is_mfma else None, rows if is_mfma else 0,
+                     XCORR_ALGOS["mfma" if is_mfma else "valu"], min_k, pc, 0, stream())
+        join = torch.cuda.Event()
+        join.record(side)
+        main.wait_event(join)
+        # the side stream's buffers are used across streams: keep them alive
+        # until the main stream has passed the join
+        for t in (fp, tmpl, out, slots, tsplit) + ((relu,) if relu is not None else ()):
+            t.record_stream(side)
 
     def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
                feats: Optional[torch.Tensor] = None):
@@ -763,48 +964,48 @@ class TMREngine:
             acc0 = None
             C0k = C0
             pc = prec_code(cfg.precision)
+            # Activation scales are PER SAMPLE (per unit for the f_TM records
+            # and the heads launch, per image for the fp half), so a unit's
+            # precision never depends on the other units' magnitudes
+            # (TMR_SPLIT_XMAX_PER_UNIT); bf16 records are unscaled
+            unscaled = cfg.precision == "bf16"
+            tm_max = None if unscaled else self._memo_absmax(f_tm, "ftm", lambda: absmax_rows(f_tm))
             if fold:
-                # records of [up2x(f); 1] (max |.| <= max(max|f|, 1): bilinear
-                # weights are convex); one activation scale per conv launch
+                # records of up2x(f) (max |.| <= max |f|: bilinear weights are
+                # convex), per image
                 xmax0 = self._feat_absmax(feats)
-                unscaled = cfg.precision == "bf16"  # no activation scales (bf16 records)
-                tm_max = None if unscaled else self._memo_absmax(f_tm, "ftm", lambda: absmax(f_tm))
                 if share:
                     # the fp half is its own launch (tmr_split_conv_store) with
-                    # its own activation scale
+                    # its own per-image scales
                     xmax1 = tm_max
                     acc0 = self._acc0_lookup(feats, split, H, W)
                     xp0 = None if acc0 is not None else \
                         pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax0, ones=False)
                 else:
-                    # ONE launch reads both sources and undoes ONE activation
-                    # scale (conv_split.hip takes one xmax per launch): both
-                    # record sets are packed with max(max|f_TM|, xmax0)
-                    xmax1 = None if unscaled else absmax(tm_max, xmax0.clone())
-                    xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xmax1,
-                                        ones=False)
+                    # ONE launch reads both sources of a tile with ONE scale:
+                    # per image, max(max|f|, max|f_TM| of its units)
+                    xs0, xmax1 = (None, None) if unscaled else scale_merge(xmax0, tm_max, ui, B)
+                    xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xs0, ones=False)
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
             else:
-                # 16-bit operand records; one activation scale per conv launch
-                # (both sources of a virtual concat share it); bf16 records
-                # are unscaled (no reductions; f_TM may be a bf16 plane)
-                unscaled = cfg.precision == "bf16"
                 if share:
-                    xmax0 = None if unscaled else absmax(fp)
+                    xmax0 = None if unscaled else absmax_rows(fp)
                     xp0 = pack_split_x(fp, ks, cfg.precision, xmax0)
-                    xmax1 = None if unscaled else absmax(f_tm)
+                    xmax1 = tm_max
+                elif src0 is not None:
+                    xs0, xmax1 = (None, None) if unscaled else scale_merge(absmax_rows(fp), tm_max, ui, B)
+                    xp0 = pack_split_x(fp, ks, cfg.precision, xs0)
                 else:
-                    xmax1 = absmax(fp) if src0 is not None and not unscaled else None
-                    xmax1 = None if unscaled else absmax(f_tm, xmax1)
-                    xp0 = pack_split_x(fp, ks, cfg.precision, xmax1) if src0 is not None else None
+                    xp0, xmax1 = None, tm_max
                 xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
+            xpu = 0 if unscaled else SPLIT_XMAX_PER_UNIT
             if share:
                 wp_fp, wp_tm, zero_b = split
                 if acc0 is None:  # acc0 in the kernel's tiled accumulator layout (private)
                     acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
                                        dtype=torch.float32)
-                    fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0)
+                    fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0) | xpu
                     if bplane is not None:
                         fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
                     call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
@@ -823,6 +1024,7 @@ class TMREngine:
             if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
                 a0 = ptr(bplane)
                 fl = SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
+            fl |= xpu
             call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                  U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
                  a0, ptr(part), fl, stream())
@@ -915,19 +1117,16 @@ class TMREngine:
         g = self._graphs.get(sig)
         self.last_graph = "replay" if g is not None else "eager"
         if g is None:
-            self._graph_seen[sig] = self._graph_seen.get(sig, 0) + 1
-            if self._graph_seen[sig] < 2:
+            if not self._graphs.want_capture(sig):
                 return None
             g = self._capture_module(feats, unit_image, boxes, want_aux, hit, self._detect_host_inputs(
                 units, unit_image, B, np.zeros(0, np.uint8)))
+            self._graphs.put(sig, g)
             if g is None:
                 return None
-            if len(self._graphs) >= self.GRAPH_CACHE:
-                self._graphs.pop(next(iter(self._graphs)))
-            self._graphs[sig] = g
             self.last_graph = "captured"
         host_in = self._detect_host_inputs(units, unit_image, B, np.zeros(0, np.uint8))
-        out = g.replay(feats.float().contiguous(), host_in)
+        out = g.replay(feats.float().contiguous(), host_in, reuse_feats=True)
         for k, v in g.last.items():
             setattr(self, k, v)
         if hit is None:  # this image's memo: the first-call graph's fp / acc0
@@ -1209,16 +1408,12 @@ class TMREngine:
         spec = (unit_off, seg.astype(np.int32), iou_threshold) if nms_in is not None else None
         g = self._graphs.get(sig) if sig is not None else None
         self.last_graph = "replay" if g is not None else "eager"
-        if g is None and sig is not None:
-            self._graph_seen[sig] = self._graph_seen.get(sig, 0) + 1
-            if self._graph_seen[sig] >= 2:
-                g = self._capture_detect(feats, unit_image, boxes, params, self._detect_host_inputs(
-                    units, unit_image, B, params, nms_in), spec)
-                if g is not None:
-                    if len(self._graphs) >= self.GRAPH_CACHE:
-                        self._graphs.pop(next(iter(self._graphs)))
-                    self._graphs[sig] = g
-                    self.last_graph = "captured"
+        if g is None and sig is not None and self._graphs.want_capture(sig):
+            g = self._capture_detect(feats, unit_image, boxes, params, self._detect_host_inputs(
+                units, unit_image, B, params, nms_in), spec)
+            self._graphs.put(sig, g)
+            if g is not None:
+                self.last_graph = "captured"
         if g is not None:
             host_in = self._detect_host_inputs(units, unit_image, B, params, nms_in)
             out = g.replay(feats.float().contiguous(), host_in)

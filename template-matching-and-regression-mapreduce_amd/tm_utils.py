@@ -83,7 +83,9 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
                    input_is_prob=False):
     """TM_utils.py:224-305.  pred_objectness: list over levels of [B,1,H,W]
     logits; pred_regressions: list of [B,4,H,W] (or None entries).
-    Returns (pred_logits, pred_boxes, ref_points): lists over images.
+    Returns (pred_logits, pred_boxes, ref_points): lists over images.  An
+    image's candidate rows are views into this call's own (fresh) peak
+    buffers, as the reference's boolean-index results are fresh tensors.
     ``input_is_prob`` (extension) feeds probability maps instead of logits,
     the form the bit-exact contract is stated on."""
     dtype = pred_objectness[-1].dtype
@@ -115,8 +117,11 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         else:
             lg = torch.cat([p[0] for p in parts]); bx = torch.cat([p[1] for p in parts])
             rf = torch.cat([p[2] for p in parts])
-        if lg.shape[0] == 0:  # every level empty: the dummy row
-            lg, bx, rf = dummies[b] if dtype == torch.float32 else _dummy(dtype, device)
+        if lg.shape[0] == 0:  # every level empty: the dummy row, fresh 1-row tensors as the
+            # reference's (TM_utils.py:288-291): cloned on the device (no sync), so a kept
+            # dummy does not hold the call's [U*H*W] peak buffers alive
+            lg, bx, rf = (tuple(t.clone() for t in dummies[b]) if dtype == torch.float32
+                          else _dummy(dtype, device))
         pred_logits.append(lg); pred_boxes.append(bx); ref_points.append(rf)
     return pred_logits, pred_boxes, ref_points
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes table out of sync with tmr.h"
     L = tmr_amd.load()
-    assert L.tmr_version() == 1
+    assert L.tmr_version() == 2
     assert L.tmr_strerror(0) == b"ok"
     assert b"invalid" in L.tmr_strerror(-1)
 
@@ -42,9 +42,12 @@ def test_size_queries_no_gpu():
     L = tmr_amd.load()
     assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
     assert L.tmr_nms_work_size(10, 4, 5, 3) > 10 * 40
-    # bounded: the IoU words of 64 images x 49,152 candidates stay within the strip budget
+    # linear in the candidates (the binned NMS keeps no n^2 IoU matrix): at most
+    # 240 B per candidate plus a fixed part, 64 images x 49,152 candidates
     big = L.tmr_nms_work_size(64 * 49152, 64 * 768, 49152, 64)
-    assert big < 64 * 49152 * 64 + (300 << 20)
+    assert big < 64 * 49152 * 240 + (16 << 20)
+    half = L.tmr_nms_work_size(32 * 49152, 32 * 768, 49152, 32)
+    assert abs(big - 2 * half) < (4 << 20)
 
 
 def test_split_size_queries_no_gpu():
@@ -80,8 +83,12 @@ def test_invalid_arguments_return_codes():
                                   None, None, None, 0, None) == -1
     assert L.tmr_split_acc_size(2, 2048, 128, 128) == 2 * 2048 * 128 * 128
     assert L.tmr_split_acc_size(1, 100, 17, 33) == 128 * 32 * 64
-    assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, None, None) == -1
+    assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, 0, None, None) == -1
     assert L.tmr_absmax(None, 4, 0, None, None) == -1
+    # per-sample scale sources (ABI 2): missing pointers / empty batches never launch
+    assert L.tmr_absmax_rows(None, 2, 4, 0, None, None) == -1
+    assert L.tmr_absmax_rows(None, 0, 4, 0, None, None) == -1
+    assert L.tmr_scale_merge(None, None, None, 2, 3, None, None, None) == -1
     # masked maxpool: an empty selection (torch.max rejects it) or bits past the 3x3 window
     assert L.tmr_maxpool3x3(None, 1, 4, 4, 0, None, None) == -1
     assert L.tmr_maxpool3x3(None, 1, 4, 4, 1 << 9, None, None) == -1
@@ -305,6 +312,7 @@ def test_build_units_vectorised_matches_scalar():
         assert (units["ht"][u], units["wt"][u]) == (ht, wt)
         assert np.array_equal(units["roi"][u].view(np.uint32), roi.view(np.uint32))
         assert units["tmpl_offset"][u] == off and units["row_offset"][u] == rows
+        assert units["out_unit"][u] == u
         off += C * ht * wt
         rows += ht * host.tsplit_nk(wt)
     assert tfl == off and mh == units["ht"].max() and mw == units["wt"].max()
@@ -320,6 +328,7 @@ def test_build_units_vectorised_matches_scalar():
         ref = units[u0:u0 + n].copy()
         ref["tmpl_offset"] -= ref["tmpl_offset"][0]
         ref["row_offset"] -= ref["row_offset"][0]
+        ref["out_unit"] -= ref["out_unit"][0]
         for f in small.dtype.names:  # field-wise (a structured copy leaves the padding undefined)
             a, b = np.ascontiguousarray(small[f]), np.ascontiguousarray(ref[f])
             assert a.tobytes() == b.tobytes(), (u0, n, f)
@@ -377,3 +386,35 @@ def test_clone_outputs_groups_views_of_one_buffer():
     nc = torch.arange(12.0).view(3, 4)[:, :2]  # non-contiguous views are cloned one by one
     r = _clone_outputs({"a": nc, "b": nc.t()})
     assert torch.equal(r["a"], nc) and torch.equal(r["b"], nc.t())
+
+
+def test_graph_book_bounded_and_failures_remembered():
+    """TMREngine's graph bookkeeping: a signature is captured on
+    its second sighting; the seen-counts and the failure set are bounded
+    LRUs (varied exemplar sizes make a new signature almost every batch);
+    a failed capture is remembered, so that signature stays eager without
+    re-trying the capture; graphs are an LRU of GRAPH_CACHE."""
+    from tmr_amd.engine import TMREngine, _GraphBook
+    b = _GraphBook(cap=2, seen_cap=4)
+    assert not b.want_capture("a") and b.want_capture("a")
+    b.put("a", "graph-a")
+    assert b.get("a") == "graph-a" and "a" not in b.seen
+    # the seen-counts stay bounded under a stream of one-off signatures
+    for i in range(100):
+        assert not b.want_capture(("once", i))
+    assert len(b.seen) == 4
+    # a failed capture: never retried
+    assert not b.want_capture("bad") and b.want_capture("bad")
+    b.put("bad", None)
+    assert all(not b.want_capture("bad") for _ in range(5)) and b.get("bad") is None
+    for i in range(10):
+        b.put(("bad", i), None)
+    assert len(b.failed) == 4
+    # graphs: LRU of cap, a hit refreshes its entry
+    b.put("b", "graph-b")
+    assert b.get("a") == "graph-a"
+    b.put("c", "graph-c")
+    assert b.get("b") is None and b.get("a") == "graph-a" and b.get("c") == "graph-c"
+    b.clear()
+    assert not (b.graphs or b.seen or b.failed)
+    assert TMREngine.GRAPH_CACHE >= 1

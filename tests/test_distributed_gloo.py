@@ -1,10 +1,13 @@
-"""Multi-process data-parallel driver on CPU (gloo, world_size 2 and 3).
+"""Multi-process data-parallel driver on CPU (gloo, world_size 2, 3 and 8).
 
 The per-rank compute here is the CPU oracle (tests may use it as the
 checker); the product's GPU run uses TMREngine.detect with the same driver
 code and the nccl (RCCL) backend.  Checks: sharding covers every image once,
 the all-gather returns every rank's detections in global image order, and
-the result equals a single-process run.
+the result equals a single-process run -- including 8 ranks (the node's GPU
+count, rehearsed on CPU) over 13 images, where ranks hold 1 or 2 images and
+(batch 1) the short ones run out and contribute empty batches to the later
+rounds' all-gathers, and over 5 images, where 3 ranks hold none at all.
 """
 import os
 import socket
@@ -48,22 +51,21 @@ def _detect_oracle(P):
     return fn
 
 
-def _setup():
+def _setup(n=7):
     P = oracle.reference_weights(0, cin=CIN, emb=EMB)
     P["objectness_head.head.0.bias"] = torch.tensor([0.3])
-    n = 7
     feats = torch.from_numpy(synth.sam_features(3, n, CIN, HF, HF))
     ex, _ = synth.exemplar_set(4, n, 2, 2 * HF, 2 * HF, 3, 5)
     return P, feats, ex, n
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, n=7, batch=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
-    P, feats, ex, n = _setup()
+    P, feats, ex, n = _setup(n)
     counts, rows = driver.run_sharded(_detect_oracle(P), lambda s, e: (feats[s:e], ex[s:e]), n,
-                                      batch=2, rank=rank, world=world)
+                                      batch=batch, rank=rank, world=world)
     q.put((rank, counts, [r.numpy() for r in rows]))
     dist.destroy_process_group()
 
@@ -76,12 +78,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_driver_gloo(world):
+@pytest.mark.parametrize("world,n,batch", [(2, 7, 2), (3, 7, 2), (8, 13, 2), (8, 13, 1), (8, 5, 1)])
+def test_sharded_driver_gloo(world, n, batch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n, batch)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -89,9 +91,9 @@ def test_sharded_driver_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     # single-process reference run
-    P, feats, ex, n = _setup()
+    P, feats, ex, n = _setup(n)
     c1, r1 = driver.run_sharded(_detect_oracle(P), lambda s, e: (feats[s:e], ex[s:e]), n,
-                                batch=2, rank=0, world=1)
+                                batch=batch, rank=0, world=1)
     assert (c1 >= 1).all()
     for rank, counts, rows in res:
         assert np.array_equal(counts, c1), rank

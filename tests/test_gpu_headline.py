@@ -142,7 +142,7 @@ FULL_BATCH = {  # bench.py's configs: (images, E, feature side, k range, precisi
 
 @pytest.mark.skipif(not os.environ.get("TMR_FULL_PARITY"),
                     reason="every image of the batch against the oracle (~1 s of CPU per unit); "
-                           "set TMR_FULL_PARITY=1 (record: profiles/r03p_full_parity.log)")
+                           "set TMR_FULL_PARITY=1 (record: profiles/archive/r03p_full_parity.log)")
 @pytest.mark.parametrize("config", sorted(FULL_BATCH))
 def test_full_batch_every_image(config):
     """bench.py configs B, C, D and E with EVERY image of the batch checked

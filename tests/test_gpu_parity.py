@@ -105,13 +105,13 @@ def test_xcorr_golden(golden):
         scale = torch.ones(1, device=DEV)
         ud = _units_to_device(units, DEV)
         iu = cuda(np.array([0, 1], np.int32))
-        amax = torch.zeros(256, device=DEV)  # TMR_ABSMAX_SLOTS
+        amax = torch.zeros(1, device=DEV)  # per-unit max |f_TM| (one unit)
         call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), ptr(iu), 1, h, w, ptr(scale), sq,
              ptr(out), ptr(relu), ptr(work) if work is not None else None, ptr(amax), stream())
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert normwise(got, ref) <= TOL, (i, normwise(got, ref))
-        assert amax.max().item() == np.abs(got).max()  # fused |f_TM| max (split decoder scale)
+        assert amax.item() == np.abs(got).max()  # fused |f_TM| max (split decoder scale)
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0))
         # the pad border is exactly zero
         if h > 1:
@@ -290,9 +290,12 @@ def _xrecords_ref(x, ks, prec, xmax):
     Hp, Wp = -(-H // 16) * 16 + ks - 1, -(-W // 32) * 32 + ks - 1
     xs = torch.zeros(S, NCc * 32, Hp, Wp, dtype=torch.float32, device=x.device)
     sc = 1.0
-    if prec != "bf16":
-        e = int(np.frexp(np.float32(xmax))[1])
-        sc = float(2.0 ** (14 - e))
+    if prec != "bf16":  # one source, one per sample [S] or one per pixel [S,H,W]
+        m = np.asarray(xmax, np.float32)
+        e = np.frexp(m)[1]
+        sc = np.where(m > 0, np.exp2(np.clip(14 - e, -63, 63)), 1.0).astype(np.float32)
+        sc = torch.from_numpy(sc.reshape((S, 1, H, W) if m.ndim == 3 else (-1, 1, 1, 1) if m.ndim else ()))
+        sc = sc.to(x.device)
     xs[:, :C, pad:pad + H, pad:pad + W] = x * sc
     dt = torch.bfloat16 if prec == "bf16" else torch.float16
     hi = xs.to(dt)
@@ -311,26 +314,30 @@ def test_xpack_records_bitexact(S, C, H, W, ks):
     kernel otherwise) bit-exact against the torch restatement of the layout,
     padding ring included (the buffer is pre-filled with garbage)."""
     from tmr_amd._lib import PREC_CODES, call, load, ptr, stream
-    from tmr_amd.engine import absmax
+    from tmr_amd.engine import absmax, absmax_rows, pixel_absmax
     torch.manual_seed(11)
-    x = (torch.randn(S, C, H, W) * 3).cuda()
-    xmax = absmax(x)
-    for prec in ("fp32", "bf16", "f16"):
-        n = load().tmr_split_xpack_size(S, C, H, W, ks, PREC_CODES[prec])
-        out = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
-        call("tmr_split_xpack", ptr(x), S, C, H, W, ks, PREC_CODES[prec], ptr(xmax), ptr(out), stream())
-        ref = _xrecords_ref(x, ks, prec, float(xmax.item()))
-        got = out.view(torch.int16)
-        assert got.numel() == ref.numel(), prec
-        bad = int((got != ref).sum())
-        assert bad == 0, f"{prec}: {bad} of {ref.numel()} 16-bit words differ"
-        if prec == "bf16" and W % 8 == 0:
-            # the bf16 input form (tmr_split_xpack16 of bf16(x), the bf16
-            # f_TM plane of tmr_xcorr_out): the same records bit for bit
-            out16 = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
-            xb = x.to(torch.bfloat16)
-            call("tmr_split_xpack16", ptr(xb), S, C, H, W, ks, PREC_CODES[prec], ptr(out16), stream())
-            assert torch.equal(out16, out), "xpack16"
+    # samples 2^20 apart and a quiet pixel block: the per-sample and per-pixel
+    # scale modes (xmax_per_sample 1 / 2) are exercised with real spread
+    x = (torch.randn(S, C, H, W) * 3 * torch.tensor([2.0 ** (-20 * s) for s in range(S)])[:, None, None, None])
+    x[0, :, : H // 2, : W // 3] *= 1e-6
+    x = x.cuda()
+    for mode, xmax in ((0, absmax(x)), (1, absmax_rows(x)), (2, pixel_absmax(x))):
+        for prec in ("fp32", "bf16", "f16"):
+            n = load().tmr_split_xpack_size(S, C, H, W, ks, PREC_CODES[prec])
+            out = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
+            call("tmr_split_xpack", ptr(x), S, C, H, W, ks, PREC_CODES[prec], ptr(xmax), mode, ptr(out), stream())
+            ref = _xrecords_ref(x, ks, prec, xmax.cpu().numpy() if mode else float(xmax.item()))
+            got = out.view(torch.int16)
+            assert got.numel() == ref.numel(), prec
+            bad = int((got != ref).sum())
+            assert bad == 0, f"{prec}: {bad} of {ref.numel()} 16-bit words differ"
+            if prec == "bf16" and W % 8 == 0:
+                # the bf16 input form (tmr_split_xpack16 of bf16(x), the bf16
+                # f_TM plane of tmr_xcorr_out): the same records bit for bit
+                out16 = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
+                xb = x.to(torch.bfloat16)
+                call("tmr_split_xpack16", ptr(xb), S, C, H, W, ks, PREC_CODES[prec], ptr(out16), stream())
+                assert torch.equal(out16, out), "xpack16"
 
 
 def test_split_acc_slab_bf16():
@@ -649,6 +656,80 @@ def test_nms_small_images_one_workgroup_path():
                     assert bits_equal(B1[0].cpu().numpy(), bx[keep]), (n, thr)
 
 
+def _nms_binned_cases():
+    """Images that stress the spatially binned NMS (csrc/nms.hip): a uniform
+    spray of small boxes, a cluster of identical boxes (every row suppresses
+    the rest: the lists overflow CAP and kept rows rescan their window),
+    tiny and huge boxes mixed, boxes touching exactly edge to edge, inverted
+    and zero-area boxes, far-from-origin coordinates, score ties."""
+    r = np.random.default_rng(77)
+    cases = []
+    n = 1500
+    xy = r.random((n, 2), np.float32) * 0.95
+    wh = (0.005 + r.random((n, 2)) * 0.04).astype(np.float32)
+    cases.append(np.concatenate([xy, xy + wh], 1))
+    base = np.array([0.4, 0.4, 0.45, 0.47], np.float32)
+    cl = np.repeat(base[None], 400, 0)
+    cl[200:] += (r.random((200, 1)) * 0.01).astype(np.float32)
+    cases.append(cl)
+    xy = r.random((n, 2), np.float32)
+    wh = np.where(r.random((n, 1)) < 0.05, 0.3 + r.random((n, 2)) * 0.6, 0.002 + r.random((n, 2)) * 0.01)
+    cases.append(np.concatenate([xy, xy + wh.astype(np.float32)], 1).astype(np.float32))
+    g = np.arange(30, dtype=np.float32) / 32.0  # a grid of unit cells touching exactly
+    gx, gy = np.meshgrid(g, g)
+    t = np.stack([gx.ravel(), gy.ravel(), gx.ravel() + 1.0 / 32.0, gy.ravel() + 1.0 / 32.0], 1)
+    t = np.concatenate([t, t[::3] + np.float32(1.0 / 64.0)])
+    cases.append(t.astype(np.float32))
+    xy = r.random((800, 2), np.float32) * 0.9
+    bx = np.concatenate([xy, xy + 0.03], 1).astype(np.float32)
+    bx[::7, 2] = bx[::7, 0] - 0.01   # inverted
+    bx[1::11, 2:] = bx[1::11, :2]    # zero area
+    cases.append(bx)
+    xy = 1000.0 + r.random((700, 2), np.float32) * 3.0
+    cases.append(np.concatenate([xy, xy + 0.05 + r.random((700, 2), np.float32) * 0.2], 1).astype(np.float32))
+    out = []
+    for k, bx in enumerate(cases):
+        sc = (np.round(r.random(len(bx)) * 32) / 32).astype(np.float32)  # ties
+        out.append((bx.astype(np.float32), sc))
+    return out
+
+
+@pytest.mark.parametrize("thr", [0.0, 0.15, 0.5, 0.9, -0.1])
+def test_nms_binned_edge_cases_vs_oracle(thr):
+    """The binned NMS (images above TMR_NMS_SMALL candidates) keeps exactly
+    the oracle's sequential torchvision list on every case, all images of
+    the call binned together (a negative threshold: one cell per image,
+    every pair evaluated)."""
+    cases = _nms_binned_cases()
+    L, Bx, R = tmr_amd.NMS([cuda(np.stack([sc, np.zeros_like(sc)], 1)) for bx, sc in cases],
+                           [cuda(bx) for bx, sc in cases], [cuda(bx[:, :2].copy()) for bx, sc in cases], thr)
+    for k, (bx, sc) in enumerate(cases):
+        keep = oracle.nms(bx, sc, thr)
+        assert bits_equal(Bx[k].cpu().numpy(), bx[keep]), (thr, k, len(keep), Bx[k].shape[0])
+        assert bits_equal(L[k].cpu().numpy()[:, 0], sc[keep]), (thr, k)
+
+
+def test_nms_binned_nonfinite_boxes_match_dense():
+    """Non-finite box coordinates put the image in one bin (every pair
+    evaluated with the kernels' own fmaxf/fminf arithmetic): an image of
+    <= 256 candidates gives the same kept rows through the one-workgroup
+    path and through the binned path (called beside a large image)."""
+    big_bx, big_sc = _nms_case(601, 900)
+    for seed in (602, 603):
+        bx, sc = _nms_case(seed, 200)
+        bx[5, 0] = np.nan
+        bx[9, 2] = np.inf
+        bx[13, 1] = -np.inf
+        lg = np.stack([sc, np.zeros_like(sc)], 1)
+        lgb = np.stack([big_sc, np.zeros_like(big_sc)], 1)
+        for thr in (0.15, 0.5):
+            L1, B1, R1 = tmr_amd.NMS([cuda(lg)], [cuda(bx)], [cuda(bx[:, :2].copy())], thr)
+            L2, B2, R2 = tmr_amd.NMS([cuda(lg), cuda(lgb)], [cuda(bx), cuda(big_bx)],
+                                     [cuda(bx[:, :2].copy()), cuda(big_bx[:, :2].copy())], thr)
+            assert bits_equal(L1[0].cpu().numpy(), L2[0].cpu().numpy()), (seed, thr)
+            assert bits_equal(B1[0].cpu().numpy(), B2[0].cpu().numpy()), (seed, thr)
+
+
 # ----------------------------------------------------------------- callers
 def test_caller_sequence_golden(golden):
     """demo.Inference.infer / each_step_multi_exemplars through TMREngine.detect."""
@@ -838,13 +919,14 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
     for algo in ("valu", "mfma"):
         out = torch.empty((U, C, H, W), device=DEV)
         relu = torch.empty_like(out)
-        amax = torch.zeros(256, device=DEV)
+        amax = torch.zeros(U, device=DEV)
         call("tmr_xcorr_prec", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
              ptr(out), ptr(relu), None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, stream())
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         outs[algo] = got
-        assert amax.max().item() == np.abs(got).max(), algo
+        # the fused per-unit max |f_TM| (the decoder's per-unit scale source)
+        assert np.array_equal(amax.cpu().numpy(), np.abs(got).reshape(U, -1).max(1)), algo
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0)), algo
         if algo == "mfma" and prec == "bf16":
             # tmr_xcorr_out's bf16 plane: RNE bf16 of the fp32 plane, bit for bit
@@ -928,6 +1010,44 @@ def test_xcorr_mfma_squeeze_and_engine():
             ref = oracle.xcorr(f[ui[u]], t, 1.25, sq)
             for algo in ("valu", "mfma", "auto"):
                 assert normwise(res[(sq, algo)][u], ref) <= TOL, (sq, algo, u)
+
+
+def test_xcorr_split_launch_matches_single_kernel_launches():
+    """TMREngine.xcorr_split: a mixed launch split per unit by the cost model
+    into a VALU launch (side stream) and an MFMA launch (current stream) over
+    complementary unit subsets (tmr_unit_t.out_unit): every unit's f_TM and
+    relu(f_TM), and its fused max |f_TM|, are bit-identical to the
+    single-kernel launch of its own kernel over the whole batch."""
+    from tmr_amd.engine import xcorr_unit_split
+    C, H, W, B, E = 32, 128, 128, 4, 3
+    P = {k: cuda(v) for k, v in synth.reference_state_dict(31, cin=16, emb=C).items()}
+    fp = cuda(synth.normal(32, (B, C, H, W)))
+    ex, ks = synth.exemplar_set(33, B, E, H, W, 3, 15)
+    boxes, ui = ex.reshape(-1, 4), np.repeat(np.arange(B), E)
+    res = {}
+    for mode in ("valu", "mfma", "split"):
+        eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C))
+        eng.xcorr_algo = "auto" if mode == "split" else mode
+        eng.xcorr_split = mode == "split"
+        if mode == "split":  # force a mixed set whatever the cost table says
+            import tmr_amd.engine as E_
+            orig = E_.xcorr_unit_split
+            E_.xcorr_unit_split = lambda ht, wt, upi, one_term=False: np.maximum(ht, wt) >= 11
+        try:
+            f, relu = eng.match(fp, ui, boxes, want_relu=True)
+        finally:
+            if mode == "split":
+                E_.xcorr_unit_split = orig
+        torch.cuda.synchronize()
+        res[mode] = (f.cpu().numpy(), relu.cpu().numpy(), eng._memo_absmax(f, "ftm").cpu().numpy(),
+                     eng.last_xcorr_algo)
+    assert res["split"][3] == "split"
+    for u in range(B * E):
+        k = max(host.template_size(boxes[u], H, W)[1:])
+        src = "mfma" if k >= 11 else "valu"
+        for t in range(3):
+            assert bits_equal(res["split"][t][u], res[src][t][u]), (u, k, t)
+    assert xcorr_unit_split(np.array([3, 15]), np.array([3, 15]), 3.0).tolist() == [False, True]
 
 
 def test_nms_worst_case_dense_candidates():

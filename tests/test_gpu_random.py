@@ -147,6 +147,19 @@ def test_random_module_variant_vs_oracle(seed):
     switch drawn at random) called in the reference's module form, against
     oracle.forward_torch with the same switches: o, b, relu(f_TM) within 1e-5
     normwise, f[0] within 1e-6 (its fma form is bit-exact with the C oracle)."""
+    _module_variant(seed, 1e-5)
+
+
+def test_cancellation_variant_margin():
+    """The module variant that retired the 6-bit hi weights (seed 188: a 1x1
+    decoder over 16 channels with heavy cancellation; 1.33e-5 at 6 bits,
+    1.5e-6 at the kept 8), held to 5e-6: a regression guard on
+    the margin of the WH_BITS = 8 weight split."""
+    assert draw_variant(188)["k"] == 1
+    _module_variant(188, 5e-6)
+
+
+def _module_variant(seed, tol):
     from types import SimpleNamespace
     c = draw_variant(seed)
     args = SimpleNamespace(emb_dim=c["emb"], fusion=c["fusion"], ablation_no_box_regression=not c["box_reg"],
@@ -176,6 +189,6 @@ def test_random_module_variant_vs_oracle(seed):
         errs.append(normwise(bs_[0].cpu().numpy(), rb[0].numpy()))
     else:
         assert bs_[0] is None
-    assert max(errs) <= 1e-5, (c, errs)
+    assert max(errs) <= tol, (c, errs)
     assert normwise(f0.cpu().numpy(), r0.numpy()) <= 1e-6, c
     print(f"variant seed {seed}: {c} worst normwise {max(errs):.2e}")

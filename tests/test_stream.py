@@ -101,7 +101,37 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rec = np.stack([np.arange(mr.REC, dtype=np.float64) + 100 * rank + 10 * j for j in range(rank % 3)]) \
+        if rank % 3 else np.zeros((0, mr.REC))
+    q.put((rank, mr.gather_records(rec)))
+    dist.destroy_process_group()
+
+
+def test_gather_records_uneven_world8_gloo():
+    """The shuffle at the node's 8 ranks, holding 0, 1 or 2 records each
+    (ranks with no shard contribute nothing): every rank receives all records
+    in rank order (reducer.py:47-92 reads them in shard order)."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = np.stack([np.arange(mr.REC, dtype=np.float64) + 100 * r + 10 * j
+                    for r in range(world) for j in range(r % 3)])
+    for r in range(world):
+        np.testing.assert_array_equal(got[r], ref)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_map_shuffle_gloo(world):
     counts = mr.shard_image_counts(SHARDS, seed=3)
     ref = mr.run_mapper(SHARDS, counts, 0, 1, _cpu_source, _cpu_stats, None, batch=4)
