@@ -104,12 +104,15 @@ int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates
 /* Same operation with the kernel chosen explicitly: TMR_XCORR_VALU (fp32
  * LDS-blocked wavefront kernels), TMR_XCORR_MFMA (row-Toeplitz implicit GEMM
  * on v_mfma_f32_16x16x32_f16 with the fp32-grade 3-term split: W % 32 == 0,
- * W <= 256, templates <= 31x31, needs tmpl_split; TMR_E_UNSUPPORTED
- * otherwise) or TMR_XCORR_AUTO (MFMA when the shape fits it, tmpl_split is
- * given and min_k -- the smallest template side in the launch -- reaches the
- * counter-chosen crossover; VALU otherwise).  tmpl_split
- * (nullable) holds tmr_template_split(templates, ..., total_rows, ...) of the
- * same templates.  tmr_xcorr(...) runs the VALU kernels. */
+ * W <= 256, templates <= 31x31; TMR_E_UNSUPPORTED otherwise) or
+ * TMR_XCORR_AUTO (MFMA when the shape fits it and min_k -- the smallest
+ * template side in the launch -- reaches the counter-chosen crossover,
+ * DESIGN.md §4.3; VALU otherwise).  tmpl_split (nullable) holds
+ * tmr_template_split(templates, ..., total_rows, ...) of the same templates:
+ * the MFMA kernel then loads its A fragments from it; NULL (TMR_PREC_F16X3
+ * only, else TMR_E_UNSUPPORTED): the kernel builds the same fragments from
+ * the templates itself (staged in LDS per unit and channel; bit-identical
+ * results).  tmr_xcorr(...) runs the VALU kernels. */
 #define TMR_XCORR_AUTO 0
 #define TMR_XCORR_VALU 1
 #define TMR_XCORR_MFMA 2
@@ -135,10 +138,13 @@ int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *temp
  * tmr_xcorr_prec (out float [U][C][H][W]); out_bf16 = 1 writes out as bf16
  * [U][C][H][W], each element the round-to-nearest-even bf16 of the fp32
  * value tmr_xcorr_prec would write -- the bf16 contract's detect path, whose
- * decoder records (tmr_split_xpack16) are those bf16 values.  out_bf16 needs
- * algo TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0 and relu_out NULL
- * (TMR_E_INVALID otherwise).  Same sources as tmr_xcorr_prec:
- * models/template_matching.py:23-41,97. */
+ * decoder records (tmr_split_xpack16) are those bf16 values.  out_bf16 = 2 +
+ * ks (ks 1/3/5/7, C % 32 == 0): `out` receives those decoder records
+ * themselves (tmr_split_xpack16's layout for a ks x ks conv: the interior;
+ * zero the ring with tmr_split_xpack_ring) -- no f_TM plane and no record
+ * pass.  out_bf16 needs algo TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0
+ * and relu_out NULL (TMR_E_INVALID otherwise).  Same sources as
+ * tmr_xcorr_prec: models/template_matching.py:23-41,97. */
 int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
                   const float *scale, int squeeze, void *out, float *relu_out, float *work,
@@ -235,6 +241,10 @@ int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec
  * of the fp32 values those bf16 elements round. */
 int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
                       void *stream);
+/* tmr_split_xpack_ring: only the zero padding ring of the records of an
+ * [S][C][H][W] input (the interior written elsewhere, e.g. by tmr_xcorr_out's
+ * record mode). */
+int tmr_split_xpack_ring(void *out, int S, int C, int H, int W, int ks, int prec, void *stream);
 /* tmr_split_xpack_up: records of [up2x(f) (upsample) or f; 1 (ones)] from the
  * SAM features f [S][Cin][Hin][Win] (sizes: tmr_split_xpack_size with
  * C = Cin + ones at the output resolution).  With tmr_split_fold_proj it
@@ -275,6 +285,11 @@ int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, con
  * magnitude (the projection: templates cut from a quiet region of an image
  * are renormalised by the correlation, template_matching.py:75,31) */
 #define TMR_SPLIT_XMAX_PER_PIXEL 64
+/* flags bits 8..15: E, the units per image (unit u of image u / E; U % E ==
+ * 0) -- the launch then runs an image's E units' blocks of one output tile
+ * back to back (image-major order; 0 or 1: unit-major).  Results are the
+ * same either way; only the order, and so the cache reuse, changes. */
+#define TMR_SPLIT_UNITS_PER_IMAGE_SHIFT 8
 /* out[s][p] = max_c |x[s][c][p]| for x [S][C][HW] */
 int tmr_pixel_absmax(const float *x, int S, int C, int64_t HW, float *out, void *stream);
 int64_t tmr_split_acc_size(int U, int N, int H, int W);

@@ -96,12 +96,21 @@ def variant_source(name: str, src: str) -> str:
         # (correct results for U % 3 == 0 with 3 units per image, e.g. config B): the 3 blocks of an
         # image at one (pixel tile, channel tile) are consecutive on one XCD, so its acc0 tile is
         # fetched from HBM once and served from L2 to the other two
+        # Only the heads launch (EPI == 1) with a unit count divisible by 3 is remapped: the store,
+        # projection and bias-plane launches (U = images, or 1) keep the unit-major order (round 5's
+        # first build remapped every launch and faulted on the bias plane's U = 1: u out of range)
         return _sub(src, """        const int per_unit = a.NT * a.MT;
         u = L / per_unit;
         const int r = L - u * per_unit;""", """        const int per_unit = a.NT * a.MT;
-        const int ub = L / (3 * per_unit), rr = L - ub * 3 * per_unit;
-        u = ub * 3 + rr % 3;
-        const int r = rr / 3;""")
+        int r;
+        if (EPI == 1 && a.U % 3 == 0) {
+            const int ub = L / (3 * per_unit), rr = L - ub * 3 * per_unit;
+            u = ub * 3 + rr % 3;
+            r = rr / 3;
+        } else {
+            u = L / per_unit;
+            r = L - u * per_unit;
+        }""")
     raise SystemExit(f"unknown variant {name}")
 
 

@@ -220,6 +220,7 @@ struct SArgs {
     float *out, *partials;
     int NC0, NC1, U, H, W, N, NT, MT, TXN, Hp, Wp, Npad, leaky;
     int flags;  // TMR_SPLIT_TILED_OUT / TMR_SPLIT_TILED_INIT
+    int EI;     // units per image of the image-major block order (1: unit-major)
 };
 
 template <int KS, int PREC>
@@ -325,9 +326,13 @@ __global__ __launch_bounds__(NTHREADS) void split_conv_kernel(SArgs a) {
     int nt, mt, u;
     {
         // one XCD wave of 32 blocks = PXG pixel tiles x NG channel tiles
+        // image-major (TMR_SPLIT_UNITS_PER_IMAGE): an image's EI units innermost,
+        // so its units' blocks at one tile run back to back on one XCD
+        // (measured, profiles/r05c: config-B heads launch 106.55 -> 105.96 ms)
         const int per_unit = a.NT * a.MT;
-        u = L / per_unit;
-        const int r = L - u * per_unit;
+        const int ub = L / (a.EI * per_unit), rr = L - ub * a.EI * per_unit;
+        u = ub * a.EI + rr % a.EI;
+        const int r = rr / a.EI;
         if (a.MT % PXG == 0 && a.NT % NG == 0) {
             // pixel tiles in groups of 8; for each group the channel tiles in
             // groups of 4: the 32 co-resident blocks of an XCD share 4 weight
@@ -1173,7 +1178,9 @@ int split_common(const void *xp0, int C0, const int32_t *unit_image, const void 
     a.Hp = pad_h(H, ks);
     a.Wp = pad_w(W, ks);
     a.leaky = leaky;
-    a.flags = flags;
+    a.flags = flags & 0xff;
+    a.EI = std::max(1, (flags >> TMR_SPLIT_UNITS_PER_IMAGE_SHIFT) & 0xff);
+    TMR_REQUIRE(U % a.EI == 0);
     hipStream_t s = tmr_stream(stream);
     return epi ? dispatch_ks<1>(ks, prec, a, s) : dispatch_ks<0>(ks, prec, a, s);
 }
@@ -1302,6 +1309,32 @@ extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int 
     hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16, __bf16, RPB>), g4, dim3(256), 0, tmr_stream(stream),
                        static_cast<const __bf16 *>(x), S, C, H, W, NCc, Hp, Wp, ks / 2, nseg, nbord, nullptr, 0,
                        static_cast<b8 *>(out));
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+extern "C" int tmr_split_xpack_ring(void *out, int S, int C, int H, int W, int ks, int prec, void *stream) {
+    TMR_REQUIRE(out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
+    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
+    const int64_t nbord = (int64_t)Hp * Wp - (int64_t)H * W;
+    const dim3 g((unsigned)tmr_cdiv(nbord * S * NCc, 256));
+    if (nbord == 0) return TMR_OK;
+    hipStream_t s = tmr_stream(stream);
+    // xpack4_kernel with no row segments: every block writes the zero ring
+    switch (prec) {
+        case TMR_PREC_F16X3:
+            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_F16X3>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
+                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<h8 *>(out));
+            break;
+        case TMR_PREC_BF16:
+            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
+                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<b8 *>(out));
+            break;
+        default:
+            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_F16>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
+                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<h8 *>(out));
+            break;
+    }
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

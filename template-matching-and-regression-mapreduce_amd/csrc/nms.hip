@@ -16,14 +16,14 @@
 //            corner lies within the other's extent + the image's largest box
 //            extent, so a box's partners are found in a small window of cells
 //   pairs  : one thread per box, in cell order (neighbours in a wave scan the
-//            same cells): the exact IoU against every later-sorted box of its
-//            window; suppressions inside its own 64-row block go to a
-//            diagonal word, later ones to a list of up to CAP entries
-//   greedy : one wave per image walks the 64-row blocks in score order: the
-//            block's chain is resolved from the diagonal words in registers,
-//            the kept rows' lists are OR-ed into the image's "removed" bitmap
-//            in LDS (a kept row with more than CAP partners rescans its
-//            window instead).  Memory is O(candidates); the work is the
+//            same cells): the exact IoU against the boxes of its window that
+//            are in earlier 64-row blocks (its possible suppressors: a list of
+//            up to CAP) or later in its own block (a diagonal word)
+//   greedy : one wave per image walks the 64-row blocks in score order: a row
+//            is removed when a listed suppressor is in the kept bitmap (LDS),
+//            then the block's chain is resolved from the diagonal words in
+//            registers (a row with more than CAP suppressors, none listed kept,
+//            rescans its window).  Memory is O(candidates); the work is the
 //            spatial pairs, not n^2/2 (round 4's dense strips: 4.3e9 IoU
 //            pairs per config-E step, 2.9 ms of mask + 2.0 ms of strip
 //            reduction).  The keep list equals the sequential torchvision
@@ -45,7 +45,7 @@ namespace {
 constexpr int64_t SORT_SLACK = 1 << 20;
 constexpr int GB = 64;            // bins per axis (at most)
 constexpr int NCELL = GB * GB;
-constexpr int CAP = 32;           // listed later-block suppressions per row
+constexpr int CAP = 128;          // listed earlier-block suppressors per row
 
 struct BinHdr {
     float x0, y0, icx, icy, wmax, hmax;
@@ -65,18 +65,21 @@ struct NmsWork {
     int32_t *cst;    // [G][NCELL + 1] cell starts (local)
     int32_t *clist;  // [T] sorted positions in cell order
     float *cbox;     // [T][4] their boxes
-    uint64_t *diag;  // [T] in-block suppression word of each sorted row
-    int32_t *lcnt;   // [T] later-block suppressions of each sorted row
-    int32_t *lst;    // [T][CAP] the first CAP of them (sorted positions)
+    uint64_t *diag;  // [T] in-block suppression word of each sorted row (later rows it suppresses)
+    int32_t *lcnt;   // [T] earlier-block suppressors of each sorted row
+    int32_t *lst;    // [sum_nb][CAP][64] the first CAP of them found (sorted positions),
+                     // per 64-row block entry-major: entry e of row i at
+                     // ((nb_off[g] + i/64) * CAP + e) * 64 + i%64
     char *temp;      // rocprim temporary storage
     int64_t temp_bytes;
+    int64_t lbuf_words;  // greedy_kernel: 64-bit words of LDS before its list buffers
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 inline int64_t sort_temp_bound(int64_t T, int G) { return 8 * T + SORT_SLACK + 64 * (int64_t)(G + 1); }
 
-inline NmsWork carve(void *work, int64_t T, int G) {
+inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int G) {
     NmsWork w;
     char *p = (char *)work;
     w.s = (float *)p; p += align256(sizeof(float) * T);
@@ -93,14 +96,14 @@ inline NmsWork carve(void *work, int64_t T, int G) {
     w.cbox = (float *)p; p += align256(sizeof(float) * 4 * T);
     w.diag = (uint64_t *)p; p += align256(sizeof(uint64_t) * T);
     w.lcnt = (int32_t *)p; p += align256(sizeof(int32_t) * T);
-    w.lst = (int32_t *)p; p += align256(sizeof(int32_t) * CAP * T);
+    w.lst = (int32_t *)p; p += align256(sizeof(int32_t) * CAP * 64 * sum_nb);
     w.temp = p;
     w.temp_bytes = sort_temp_bound(T, G);
     return w;
 }
 
-inline int64_t work_bytes(int64_t T, int G) {
-    const NmsWork w = carve(nullptr, T, G);
+inline int64_t work_bytes(int64_t T, int64_t sum_nb, int G) {
+    const NmsWork w = carve(nullptr, T, sum_nb, G);
     return (int64_t)(w.temp - (char *)nullptr) + w.temp_bytes + 256;
 }
 
@@ -226,7 +229,8 @@ __global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restric
 
 __device__ __forceinline__ int cell_of(float v, float v0, float ic, int gn) {
     const float c = floorf((v - v0) * ic);
-    return c < 0.0f ? 0 : c >= (float)(gn - 1) ? gn - 1 : (int)c;  // (NaN: gn - 1)
+    if (!(c >= 0.0f)) return 0;  // (below the grid, or NaN)
+    return c >= (float)(gn - 1) ? gn - 1 : (int)c;
 }
 
 // per sorted box: its cell; counting pass (MODE 0) or the fill (MODE 1)
@@ -298,7 +302,8 @@ __device__ __forceinline__ void window(const BinHdr &h, float4 bi, int &ax0, int
 }
 
 // one thread per box of image blockIdx.y, taken in cell order
-__global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ cand_off, double thr, NmsWork w) {
+__global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ cand_off,
+                                                    const int64_t *__restrict__ nb_off, double thr, NmsWork w) {
     const int g = blockIdx.y;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
@@ -309,11 +314,11 @@ __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ 
     const int i = w.clist[off + k];
     const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + i];
     const float ai = box_area(bi);
-    const int blk_end = (i | 63) + 1;  // first sorted row of the next 64-row block
+    const int blk0 = i & ~63, blk1 = blk0 + 64;  // this row's 64-row block
     const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
     const int32_t *cl = w.clist + off;
     const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
-    int32_t *lst = w.lst + (off + i) * CAP;
+    int32_t *lst = w.lst + (size_t)(nb_off[g] + (i >> 6)) * CAP * 64 + (i & 63);  // entry e at lst[e * 64]
     uint64_t diag = 0;
     int cnt = 0;
     int ax0, ax1, ay0, ay1;
@@ -322,13 +327,15 @@ __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ 
         const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];  // the window row's cells are contiguous
         for (int e = e0; e < e1; ++e) {
             const int j = cl[e];
-            if (j <= i) continue;
+            // earlier blocks: j may suppress i; later rows of this block: i may
+            // suppress j (the chain); the rest is the other row's business
+            if (j >= blk1 || (j >= blk0 && j <= i)) continue;
             const float4 bj = cb[e];
             if (!iou_over(bi, ai, bj, box_area(bj), thr, prune)) continue;
-            if (j < blk_end) {
+            if (j > i) {
                 diag |= 1ull << (j & 63);
             } else {
-                if (cnt < CAP) lst[cnt] = j;
+                if (cnt < CAP) lst[cnt * 64] = j;
                 ++cnt;
             }
         }
@@ -338,41 +345,87 @@ __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ 
 }
 
 // One wave per image: the greedy pass over the 64-row blocks in score order.
-__global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ cand_off, double thr, NmsWork w,
+// A row is removed when one of its earlier-block suppressors was kept (a
+// bitmap of the kept rows in LDS; each lane tests its own row's list, LDS
+// reads, no scatter), then the block's chain is resolved from the diagonal
+// words in registers.  A block's lists (CAP x 64 entries, entry-major, so
+// lane r reads column r conflict free) arrive in LDS by buffer-to-LDS DMA one
+// block ahead.  A row with more than CAP earlier suppressors, none of its
+// listed ones kept, is settled by the wave rescanning its window (rare).
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+constexpr int LBLK = CAP * 64;              // list entries per 64-row block
+constexpr int LDMA = LBLK * 4 / 1024;       // 1-KB DMA wave-instructions per block
+
+__device__ __forceinline__ void lists_dma(__amdgpu_buffer_rsrc_t r, int32_t *dst, int ib, int lane) {
+#pragma unroll 8
+    for (int q = 0; q < LDMA; ++q)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * 256), 16, lane * 16,
+                                                 (uint32_t)ib * (LBLK * 4) + q * 1024, 0, 0);
+}
+
+__global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ cand_off,
+                                                    const int64_t *__restrict__ nb_off, double thr, NmsWork w,
                                                     float *__restrict__ out_logits, float *__restrict__ out_boxes,
                                                     float *__restrict__ out_refs, int64_t *__restrict__ out_keep,
                                                     int32_t *__restrict__ kept_out) {
-    extern __shared__ unsigned long long removed[];
+    extern __shared__ __attribute__((aligned(16))) unsigned long long keptb[];  // [nb], then 2 list buffers
     const int g = blockIdx.x, lane = threadIdx.x;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
+    int32_t *lbuf = reinterpret_cast<int32_t *>(keptb + w.lbuf_words);  // [2][LBLK], 16-B aligned
     const BinHdr h = w.hdr[g];
     const bool prune = thr >= 0.0;
-    for (int k = lane; k < nb; k += 64) {
-        const int rem = n - k * 64;
-        removed[k] = rem >= 64 ? 0ull : ~((1ull << rem) - 1);  // rows past n never kept
-    }
     const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
     const int32_t *cl = w.clist + off;
     const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
+    const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(w.lst + (size_t)nb_off[g] * LBLK), (short)0, (int)((size_t)nb * LBLK * 4), 0x00020000);
     int cnt = 0;
-    // the next block's diagonal word and list count, loaded one block ahead
-    uint64_t dnext = lane < n ? w.diag[off + lane] : 0ull;
-    int lnext = lane < n ? w.lcnt[off + lane] : 0;
+    uint64_t diag = lane < n ? w.diag[off + lane] : 0ull;
+    int lc = lane < n ? w.lcnt[off + lane] : 0;
+    lists_dma(lr, lbuf, 0, lane);
     for (int ib = 0; ib < nb; ++ib) {
         const int i = ib * 64 + lane;
-        const uint64_t diag = dnext;
-        const int lc = lnext;
-        if (i + 64 < n) {
-            dnext = w.diag[off + i + 64];
-            lnext = w.lcnt[off + i + 64];
-        } else {
-            dnext = 0ull;
-            lnext = 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block ib's lists (and registers) are in
+        uint64_t dnext = 0ull;
+        int lnext = 0;
+        if (ib + 1 < nb) {  // the next block, in flight meanwhile
+            lists_dma(lr, lbuf + ((ib + 1) & 1) * LBLK, ib + 1, lane);
+            if (i + 64 < n) {
+                dnext = w.diag[off + i + 64];
+                lnext = w.lcnt[off + i + 64];
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint64_t word = removed[ib];
+        // removed by a kept earlier-block suppressor?
+        const int32_t *lb = lbuf + (ib & 1) * LBLK + lane;
+        const int m = i < n ? min(lc, CAP) : 0;
+        bool rem = false;
+        for (int e = 0; e < m; ++e) {
+            const int j = lb[e * 64];
+            rem |= (keptb[j >> 6] >> (j & 63)) & 1ull;
+        }
+        // more suppressors than listed and none of the listed kept: rescan
+        for (uint64_t ovf = __ballot(i < n && lc > CAP && !rem); ovf; ovf &= ovf - 1) {
+            const int r = __builtin_ctzll(ovf);
+            const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + ib * 64 + r];
+            const float ai = box_area(bi);
+            int ax0, ax1, ay0, ay1;
+            window(h, bi, ax0, ax1, ay0, ay1);
+            bool hit = false;
+            for (int ay = ay0; ay <= ay1; ++ay) {
+                const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];
+                for (int e = e0 + lane; e < e1; e += 64) {
+                    const int j = cl[e];
+                    if (j >= ib * 64 || !((keptb[j >> 6] >> (j & 63)) & 1ull)) continue;
+                    hit |= iou_over(bi, ai, cb[e], box_area(cb[e]), thr, prune);
+                }
+            }
+            if (__ballot(hit) && lane == r) rem = true;
+        }
+        uint64_t word = __ballot(rem);
+        const int rows = n - ib * 64;
+        if (rows < 64) word |= ~((1ull << rows) - 1);  // rows past n never kept
         uint64_t kept = 0;
         const uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
         for (uint64_t avail = ~word; avail;) {  // the surviving rows, lowest first
@@ -383,8 +436,8 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
             word |= ((uint64_t)hi << 32) | lo;
             avail = bit == 63 ? 0ull : ~word & (~0ull << (bit + 1));
         }
-        const bool mine = (kept >> lane) & 1ull;
-        if (mine) {
+        if (lane == 0) keptb[ib] = kept;
+        if ((kept >> lane) & 1ull) {
             const int pos = cnt + __popcll(kept & ((1ull << lane) - 1));
             const int li = min(max(w.order[off + i], 0), n - 1);
             const int64_t src = off + li, dst = off + pos;
@@ -396,33 +449,11 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
             if (out_keep) out_keep[dst] = li;
         }
         cnt += __popcll(kept);
-        // the kept rows' later-block suppressions into the bitmap
-        const int m = mine ? min(lc, CAP) : 0;
-        const int32_t *li_ = w.lst + (off + i) * CAP;
-        for (int e = 0; e < m; ++e) {
-            const int j = li_[e];
-            atomicOr(&removed[j >> 6], 1ull << (j & 63));
-        }
-        // a kept row with more than CAP: the wave rescans its window
-        for (uint64_t ovf = __ballot(mine && lc > CAP); ovf; ovf &= ovf - 1) {
-            const int r = __builtin_ctzll(ovf);
-            const int ir = ib * 64 + r;
-            const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + ir];
-            const float ai = box_area(bi);
-            int ax0, ax1, ay0, ay1;
-            window(h, bi, ax0, ax1, ay0, ay1);
-            for (int ay = ay0; ay <= ay1; ++ay) {
-                const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];
-                for (int e = e0 + lane; e < e1; e += 64) {
-                    const int j = cl[e];
-                    if (j < (ib + 1) * 64) continue;
-                    if (iou_over(bi, ai, cb[e], box_area(cb[e]), thr, prune))
-                        atomicOr(&removed[j >> 6], 1ull << (j & 63));
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // keptb[ib] before the next block's reads
+        diag = dnext;
+        lc = lnext;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) kept_out[g] = cnt;
 }
 
@@ -582,7 +613,7 @@ __global__ __launch_bounds__(SMALL_N) void nms_small_dev_kernel(
 
 extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
     if (total_cand < 0 || sum_nb < 0 || max_cand < 0 || G <= 0) return -1;
-    return work_bytes(total_cand, G);
+    return work_bytes(total_cand, sum_nb, G);
 }
 
 extern "C" int tmr_nms_small(const float *logits, const float *box, const float *ref, const int32_t *counts,
@@ -610,7 +641,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     TMR_REQUIRE(total_cand < (1ll << 31));
     const int64_t max_nb = (max_cand + 63) / 64;
     TMR_REQUIRE(max_nb < (1 << 20) && G < 65536);
-    TMR_REQUIRE(max_nb * 8 <= 150 * 1024);  // the removed bitmap in LDS
+    TMR_REQUIRE(max_nb * 8 <= 90 * 1024);  // the kept bitmap in LDS (beside 64 KB of list buffers)
     hipStream_t s = tmr_stream(stream);
     if (max_cand <= SMALL_N) {  // every image fits one workgroup
         hipLaunchKernelGGL(nms_small_kernel, dim3(G), dim3(SMALL_N), 0, s, logits, box, ref, counts, unit_off,
@@ -618,7 +649,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
         TMR_CHECK_LAUNCH();
         return TMR_OK;
     }
-    NmsWork w = carve(work, total_cand, G);
+    NmsWork w = carve(work, total_cand, sum_nb, G);
     hipLaunchKernelGGL(gather_kernel, dim3(G), dim3(256), 0, s, logits, box, ref, counts, unit_off,
                        seg_units, cand_off, w);
     TMR_CHECK_LAUNCH();
@@ -645,11 +676,14 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     hipLaunchKernelGGL(bin_kernel<1>, per_box, dim3(256), 0, s, cand_off, w);
     TMR_CHECK_LAUNCH();
     hipLaunchKernelGGL(pairs_kernel, dim3((unsigned)tmr_cdiv(max_cand, 256), G), dim3(256), 0, s, cand_off,
-                       iou_threshold, w);
+                       nb_off, iou_threshold, w);
     TMR_CHECK_LAUNCH();
-    const size_t lds = sizeof(uint64_t) * (size_t)max_nb;
+    // LDS: the kept bitmap (max_nb words, rounded to 16 B) + two list buffers
+    w.lbuf_words = (max_nb + 1) & ~int64_t(1);
+    const size_t lds = sizeof(uint64_t) * (size_t)w.lbuf_words + 2 * sizeof(int32_t) * LBLK;
+    TMR_REQUIRE(lds <= 160 * 1024);
     if (lds > 64 * 1024 && tmr_set_max_lds((const void *)greedy_kernel, lds) != hipSuccess) return TMR_E_HIP;
-    hipLaunchKernelGGL(greedy_kernel, dim3(G), dim3(64), lds, s, cand_off, iou_threshold, w, out_logits,
+    hipLaunchKernelGGL(greedy_kernel, dim3(G), dim3(64), lds, s, cand_off, nb_off, iou_threshold, w, out_logits,
                        out_boxes, out_refs, out_keep, kept);
     TMR_CHECK_LAUNCH();
     return TMR_OK;

@@ -147,25 +147,18 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o,
                 wbase += k < wave ? c : 0;
                 tot += c;
             }
-            if (f) {
-                const int y = r0 + ly - 1, pi = y * W + x;
+            if (f) {  // the slot's pixel index rides in the box row until decode_kernel
+                const int y = r0 + ly - 1;
                 const size_t k = (size_t)u * cap + base + wbase + slot;
-                const float rx = (float)x / (float)W, ry = (float)y / (float)H;
-                float r0v = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
-                if (pp.mode != 2 && r) {
-                    r0v = r[pi]; r1 = r[HW + pi]; r2 = r[2 * HW + pi]; r3 = r[3 * HW + pi];
-                }
-                const float cx = rx + r0v * sx, cy = ry + r1 * sy;
-                const float w = expf_ref(r2, et) * pp.scale_w, h = expf_ref(r3, et) * pp.scale_h;
-                const float hw2 = w / 2.0f, hh2 = h / 2.0f;
                 *reinterpret_cast<float2 *>(logits + 2 * k) = float2{v, 0.0f};
-                *reinterpret_cast<float4 *>(box + 4 * k) = float4{cx - hw2, cy - hh2, cx + hw2, cy + hh2};
-                *reinterpret_cast<float2 *>(ref + 2 * k) = float2{rx, ry};
+                reinterpret_cast<int *>(box)[4 * k] = y * W + x;
+                *reinterpret_cast<float2 *>(ref + 2 * k) = float2{(float)x / (float)W, (float)y / (float)H};
             }
             base += tot;
             __syncthreads();  // wcnt (and, after the last step, sp) free again
         }
     }
+    (void)r; (void)sx; (void)sy;
     if (tid == 0) {
         counts[u] = base;
         if (base == 0) {  // the empty unit's dummy row (TM_utils.py:288-291) at row 0
@@ -173,6 +166,35 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o,
             *reinterpret_cast<float4 *>(box + (size_t)u * cap * 4) = float4{0.0f, 0.0f, 1e-14f, 1e-14f};
             *reinterpret_cast<float2 *>(ref + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
         }
+    }
+}
+
+// The box decode of every candidate (TM_utils.py:264-278), chip-wide: one
+// thread per candidate, so the reference-exp table's binary search (a chain
+// of dependent loads) overlaps across thousands of threads instead of
+// serialising the peak finder's 64-pixel steps.
+__global__ __launch_bounds__(256) void decode_kernel(const float *__restrict__ reg, int H, int W,
+                                                     const tmr_peak_param_t *__restrict__ params,
+                                                     const int32_t *__restrict__ counts, const float *__restrict__ ref,
+                                                     float *__restrict__ box, ExpTable et) {
+    const int u = blockIdx.x;
+    const int n = counts[u];
+    const int HW = H * W;
+    const tmr_peak_param_t pp = params[u];
+    const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
+    const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < n; i += gridDim.y * 256) {
+        const size_t k = (size_t)u * HW + i;
+        const int pi = reinterpret_cast<const int *>(box)[4 * k];
+        const float2 rf = *reinterpret_cast<const float2 *>(ref + 2 * k);
+        float r0v = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+        if (pp.mode != 2 && r) {
+            r0v = r[pi]; r1 = r[HW + pi]; r2 = r[2 * HW + pi]; r3 = r[3 * HW + pi];
+        }
+        const float cx = rf.x + r0v * sx, cy = rf.y + r1 * sy;
+        const float w = expf_ref(r2, et) * pp.scale_w, h = expf_ref(r3, et) * pp.scale_h;
+        const float hw2 = w / 2.0f, hh2 = h / 2.0f;
+        *reinterpret_cast<float4 *>(box + 4 * k) = float4{cx - hw2, cy - hh2, cx + hw2, cy + hh2};
     }
 }
 
@@ -207,6 +229,9 @@ extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *
     if (lds > 64 * 1024 && tmr_set_max_lds((const void *)peaks_kernel, lds) != hipSuccess) return TMR_E_HIP;
     hipLaunchKernelGGL(peaks_kernel, dim3(U), dim3(PNT), lds, s, o, input_is_prob, reg, H, W, params, prob,
                        logits, box, ref, counts, et);
+    TMR_CHECK_LAUNCH();
+    const int ny = (int)std::min<int64_t>(tmr_cdiv((int64_t)H * W, 256), 32);
+    hipLaunchKernelGGL(decode_kernel, dim3(U, ny), dim3(256), 0, s, reg, H, W, params, counts, ref, box, et);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }

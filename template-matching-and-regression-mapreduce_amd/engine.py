@@ -32,7 +32,8 @@ import torch
 
 from . import exp_table, host
 from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
-                   SPLIT_TILED_OUT, SPLIT_XMAX_PER_PIXEL, SPLIT_XMAX_PER_UNIT, UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr,
+                   SPLIT_TILED_OUT, SPLIT_UNITS_PER_IMAGE_SHIFT, SPLIT_XMAX_PER_PIXEL, SPLIT_XMAX_PER_UNIT,
+                   UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr,
                    require_gpu, stream)
 
 NHEAD = 5
@@ -376,6 +377,17 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     return out
 
 
+class FtmRecords:
+    """f_TM as the decoder's bf16 operand records, written by the correlation
+    kernel itself (tmr_xcorr_out's record mode, the bf16 contract's detect
+    path): what TMREngine.decode would otherwise pack f_TM into."""
+
+    def __init__(self, records: torch.Tensor, shape, ks: int):
+        self.records, self.shape, self.ks = records, tuple(shape), ks
+        self.device = records.device
+        self.dtype = torch.bfloat16
+
+
 # graph capture of TMREngine.detect's forward (_DetectGraph): while set, every
 # tagged host input staged by _h2d is a view of the capture's _HostBlob
 _capture = threading.local()
@@ -582,14 +594,24 @@ class TMREngine:
         self.last_xcorr_algo = None
         # "auto" correlation of a mixed launch split by kernel per unit: the
         # units the MFMA kernel wins on run it, the others the VALU kernel,
-        # the two launches on two streams (subset launches: tmr_unit_t.out_unit)
-        self.xcorr_split = False
+        # the two launches on two streams (subset launches: tmr_unit_t.out_unit).
+        # "auto": only when images hold about one unit each -- with several
+        # units per image the split loses the band staging they share
+        # (measured, profiles/r05b/xcorr_split_ab.json: config B 5.09 -> 5.38 ms,
+        # C 2.99 -> 3.56, E equal; D, one unit per image, 2.38 -> 2.19 ms)
+        self.xcorr_split = "auto"
         self._side = None
+        # the MFMA correlation's template operands: "split" (tmr_template_split
+        # pre-expands the A fragments in HBM) or "lds" (the kernel builds them
+        # from the LDS-staged template; bit-identical)
+        self.xcorr_afrag = os.environ.get("TMR_XCORR_AFRAG", "split")
         self.last_nms_small = False  # detect: the kept rows came from the in-forward small NMS
         # bf16 contract, detect path: the one-term MFMA correlation writes
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
         self.last_xcorr_out16 = False
+        # ... and as the decoder's records themselves (no plane, no record pass)
+        self.out_records = True
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
@@ -791,7 +813,7 @@ class TMREngine:
         return fp, f0
 
     def match(self, fp: torch.Tensor, unit_image: Sequence[int], unit_boxes: np.ndarray,
-              want_relu: bool = False, allow_bf16: bool = False):
+              want_relu: bool = False, allow_bf16: bool = False, records_ks: Optional[int] = None):
         """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu).
         allow_bf16: the caller only packs f_TM into bf16 decoder records (the
         bf16 contract's detect path), so the one-term bf16 MFMA kernel may
@@ -828,7 +850,9 @@ class TMREngine:
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
         split = None
-        if self.xcorr_split and self.xcorr_algo == "auto" and fits and not cfg.squeeze and \
+        upi = U / max(1, len(set(unit_image)))
+        want_split = self.xcorr_split is True or (self.xcorr_split == "auto" and upi < 1.5)
+        if want_split and self.xcorr_algo == "auto" and fits and not cfg.squeeze and \
                 getattr(_capture, "blob", None) is None and U > 1:
             mf = xcorr_unit_split(units["ht"], units["wt"], U / max(1, len(set(unit_image))),
                                   one_term=pc != PREC_CODES["fp32"])
@@ -839,13 +863,19 @@ class TMREngine:
         out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
                  and not cfg.squeeze and not want_relu and W % 8 == 0 and split is None)
         self.last_xcorr_out16 = out16
-        out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
+        rec = out16 and records_ks is not None and self.out_records and C % 32 == 0
+        if rec:  # the decoder's bf16 records straight from the correlation epilogue
+            n = load().tmr_split_xpack_size(U, C, H, W, records_ks, pc)
+            out = torch.empty(n, device=dev, dtype=torch.uint8)
+            call("tmr_split_xpack_ring", ptr(out), U, C, H, W, records_ks, pc, stream())
+        else:
+            out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
         relu = torch.empty_like(out) if want_relu else None
         tsplit = None
         if split is not None:
             self._match_split(fp, tmpl, units, unit_image, split, scale, out, relu, slots, pc)
         else:
-            if algo != XCORR_ALGOS["valu"] and tfl > 0:
+            if algo != XCORR_ALGOS["valu"] and tfl > 0 and not self._lds_afrag(pc):
                 # the MFMA correlation's template operands (per (unit, channel) scale)
                 rows = host.tsplit_rows(units)
                 tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
@@ -854,7 +884,7 @@ class TMREngine:
                  mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
                  ptr(work) if work is not None else None, ptr(slots),
                  ptr(tsplit) if tsplit is not None else None, rows if tsplit is not None else 0, algo, min_k, pc,
-                 int(out16), stream())
+                 (2 + records_ks) if rec else int(out16), stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
@@ -872,8 +902,14 @@ class TMREngine:
             ui_ = np.asarray(unit_image)
             nimg = len(set(ui_[split].tolist())) + len(set(ui_[~split].tolist()))
         self.last_xcorr_dram_bytes = float(C * H * W) * (4.0 * nimg + (2.0 if out16 else 4.0) * U)
+        if rec:
+            return FtmRecords(out, (U, Co, H, W), records_ks), relu
         self._memo_absmax(out, "ftm", lambda: slots)
         return out, relu
+
+    def _lds_afrag(self, pc: int) -> bool:
+        """The MFMA correlation builds its A fragments in-kernel (3-term only)."""
+        return self.xcorr_afrag == "lds" and pc == PREC_CODES["fp32"]
 
     def _match_split(self, fp, tmpl, units, unit_image, mfma_units, scale, out, relu, slots, pc):
         """The correlation as two launches over complementary unit subsets
@@ -898,7 +934,9 @@ class TMREngine:
             sub_ui = ui[idx]
             subs.append((is_mfma, sub, sub_ui))
         rows = host.tsplit_rows(units)  # absolute row offsets: the full set's buffer
-        tsplit = torch.empty(load().tmr_template_split_size(len(units), C, rows), device=dev, dtype=torch.uint8)
+        lds_a = self._lds_afrag(pc)  # (the kernel builds its A fragments)
+        tsplit = None if lds_a else \
+            torch.empty(load().tmr_template_split_size(len(units), C, rows), device=dev, dtype=torch.uint8)
         for is_mfma, sub, sub_ui in subs:
             st = main if is_mfma else side
             with torch.cuda.stream(st):
@@ -908,19 +946,20 @@ class TMREngine:
                 iu_d = _h2d(host.image_ranges(sub_ui, B), dev)
                 mh, mw = int(sub["ht"].max()), int(sub["wt"].max())
                 min_k = int(min(sub["ht"].min(), sub["wt"].min()))
-                if is_mfma:
+                if is_mfma and tsplit is not None:
                     call("tmr_template_split_prec", ptr(tmpl), ptr(sub_d), len(sub), C, rows, pc, ptr(tsplit),
                          stream())
                 call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(sub_d), ptr(iu_d), len(sub), mh, mw,
                      ptr(scale), 0, ptr(out), ptr(relu) if relu is not None else None, None, ptr(slots),
-                     ptr(tsplit) if is_mfma else None, rows if is_mfma else 0,
+                     ptr(tsplit) if is_mfma and tsplit is not None else None,
+                     rows if is_mfma and tsplit is not None else 0,
                      XCORR_ALGOS["mfma" if is_mfma else "valu"], min_k, pc, 0, stream())
         join = torch.cuda.Event()
         join.record(side)
         main.wait_event(join)
         # the side stream's buffers are used across streams: keep them alive
         # until the main stream has passed the join
-        for t in (fp, tmpl, out, slots, tsplit) + ((relu,) if relu is not None else ()):
+        for t in (fp, tmpl, out, slots) + tuple(x for x in (tsplit, relu) if x is not None):
             t.record_stream(side)
 
     def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
@@ -986,7 +1025,7 @@ class TMREngine:
                     # per image, max(max|f|, max|f_TM| of its units)
                     xs0, xmax1 = (None, None) if unscaled else scale_merge(xmax0, tm_max, ui, B)
                     xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xs0, ones=False)
-                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
+                xp1 = f_tm.records if isinstance(f_tm, FtmRecords) else pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
             else:
                 if share:
@@ -998,7 +1037,7 @@ class TMREngine:
                     xp0 = pack_split_x(fp, ks, cfg.precision, xs0)
                 else:
                     xp0, xmax1 = None, tm_max
-                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
+                xp1 = f_tm.records if isinstance(f_tm, FtmRecords) else pack_split_x(f_tm, ks, cfg.precision, xmax1)
             xpu = 0 if unscaled else SPLIT_XMAX_PER_UNIT
             if share:
                 wp_fp, wp_tm, zero_b = split
@@ -1024,7 +1063,7 @@ class TMREngine:
             if acc0 is None and bplane is not None:  # unshared folded fp half: its bias plane
                 a0 = ptr(bplane)
                 fl = SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
-            fl |= xpu
+            fl |= xpu | (self._units_per_image(unit_image, B) << SPLIT_UNITS_PER_IMAGE_SHIFT)
             call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                  U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
                  a0, ptr(part), fl, stream())
@@ -1059,6 +1098,17 @@ class TMREngine:
             lw, lb = self.P["ltrbs_head.head.0.weight"], self.P["ltrbs_head.head.0.bias"]
             b = self._conv("ltrbs", res["decoder_b"], lw, lb, False)
         return o, b
+
+    @staticmethod
+    def _units_per_image(unit_image, B: int) -> int:
+        """E when the units are E per image in image order (the heads launch
+        then runs image-major, TMR_SPLIT_UNITS_PER_IMAGE_SHIFT), else 1."""
+        U = len(unit_image)
+        E = U // max(B, 1)
+        if E <= 1 or E > 255 or E * B != U:
+            return 1
+        ui = np.asarray(unit_image)
+        return E if np.array_equal(ui, np.repeat(np.arange(B), E)) else 1
 
     # ---------------------------------------------------- per-image reuse
     def _same_image(self, memo, feats: torch.Tensor) -> bool:
@@ -1205,7 +1255,8 @@ class TMREngine:
             # records and nothing else reads it
             split1 = self.cfg.decoder_num_layer == 1
             f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux,
-                                    allow_bf16=split1 and not want_aux)
+                                    allow_bf16=split1 and not want_aux,
+                                    records_ks=self.cfg.decoder_kernel_size if split1 and not want_aux else None)
         o, b = self.decode(fp, f_tm, unit_image, feats)
         return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
 

@@ -141,6 +141,10 @@ class TemplateMatching(nn.Module):
         if scale is None:
             scale = torch.ones(1, device=sample.device, dtype=torch.float32)
         eng = TMREngine({"matcher.scale": scale}, cfg)
+        # one kernel for the whole launch (no per-unit split): the batched
+        # matcher then equals its own cross_correlation member bit for bit
+        # when the cost model picks the VALU kernel, as the member runs
+        eng.xcorr_split = False
         out, _ = eng.match(sample.float().contiguous(), list(range(B)), boxes)
         return out
 

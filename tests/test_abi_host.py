@@ -43,9 +43,10 @@ def test_size_queries_no_gpu():
     assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
     assert L.tmr_nms_work_size(10, 4, 5, 3) > 10 * 40
     # linear in the candidates (the binned NMS keeps no n^2 IoU matrix): at most
-    # 240 B per candidate plus a fixed part, 64 images x 49,152 candidates
+    # 640 B per candidate (a 128-entry suppressor list is 512 of them) plus a
+    # fixed part, 64 images x 49,152 candidates
     big = L.tmr_nms_work_size(64 * 49152, 64 * 768, 49152, 64)
-    assert big < 64 * 49152 * 240 + (16 << 20)
+    assert big < 64 * 49152 * 640 + (16 << 20)
     half = L.tmr_nms_work_size(32 * 49152, 32 * 768, 49152, 32)
     assert abs(big - 2 * half) < (4 << 20)
 

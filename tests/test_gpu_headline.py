@@ -179,8 +179,9 @@ def test_config_e_last_image():
 @pytest.mark.parametrize("scale", [64.0, 1000.0])
 def test_unshared_folded_path_large_ftm(scale):
     """E = 1 (U < 2B): one split-conv launch reads the folded fp-half records and
-    the f_TM records under ONE activation scale; |f_TM| (matcher.scale) far
-    above max(1, |features|) must not bias the fp half."""
+    the f_TM records under ONE activation scale per image (tmr_scale_merge of
+    max |f| and its units' max |f_TM|); |f_TM| (matcher.scale) far above
+    max(1, |features|) must not bias the fp half."""
     B, E, hf, cin, emb = 3, 1, 16, 64, 128
     P = synth.reference_state_dict(5, cin=cin, emb=emb, obj_bias=-0.2)
     P["matcher.scale"] = torch.tensor([scale])
@@ -194,9 +195,10 @@ def test_unshared_folded_path_large_ftm(scale):
         r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
         assert eng.last_shared_flops == 0.0
         res[share] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
-        # max |f_TM| (fused in the xcorr kernel) lies exponents above max(1, |features|)
+        # max |f_TM| per unit (fused in the xcorr kernel) lies exponents above max(1, |features|)
         tm = [v[2] for k, v in eng._absmax_memo.items() if k[1] == "ftm"]
-        assert float(tm[0]) > 2.0 ** np.ceil(np.log2(max(1.0, float(np.abs(feats).max()))))
+        assert tm[0].numel() == B * E
+        assert float(tm[0].min()) > 2.0 ** np.ceil(np.log2(max(1.0, float(np.abs(feats).max()))))
     o, b = res[True]
     for u in range(B * E):
         ro, rb, _, _ = oracle.forward_torch(torch.from_numpy(feats[ui[u]:ui[u] + 1]),

@@ -964,26 +964,32 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
 
 def test_engine_bf16_ftm_plane_bitexact():
     """Under the bf16 contract the detect path's correlation writes f_TM as
-    bf16 (tmr_xcorr_out) and the decoder packs it with tmr_split_xpack16: the
-    maps are bit-identical to the fp32-plane path (engine.out_bf16 = False),
-    for the shared (E = 3) and the unshared (E = 1) fp half."""
+    bf16 (tmr_xcorr_out) -- as a plane the decoder packs with
+    tmr_split_xpack16, or as the decoder's records themselves (the record
+    mode, the ring zeroed by tmr_split_xpack_ring): the maps are
+    bit-identical to the fp32-plane path (engine.out_bf16 = False), for the
+    shared (E = 3) and the unshared (E = 1) fp half, decoder kernel sizes 3
+    and 5."""
     cin, emb, hf = 64, 128, 32
-    P = synth.reference_state_dict(9, cin=cin, emb=emb, obj_bias=-0.3)
-    for B, E in ((2, 3), (3, 1)):
-        feats = synth.sam_features(70 + E, B, cin, hf, hf)
-        ex, _ = synth.exemplar_set(71 + E, B, E, 2 * hf, 2 * hf, 3, 15)
-        ui = np.repeat(np.arange(B), E)
-        res = {}
-        for o16 in (False, True):
-            eng = tmr_amd.TMREngine({k: cuda(v) for k, v in P.items()},
-                                    tmr_amd.PathConfig(emb_dim=emb, precision="bf16"))
-            eng.xcorr_algo = "mfma"
-            eng.out_bf16 = o16
-            r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
-            assert eng.last_xcorr_out16 == o16
-            res[o16] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
-        for a, b in zip(res[False], res[True]):
-            assert bits_equal(a, b), (B, E)
+    for k in (3, 5):
+        P = synth.reference_state_dict(9, cin=cin, emb=emb, obj_bias=-0.3, k=k)
+        for B, E in ((2, 3), (3, 1)):
+            feats = synth.sam_features(70 + E, B, cin, hf, hf)
+            ex, _ = synth.exemplar_set(71 + E, B, E, 2 * hf, 2 * hf, 3, 15)
+            ui = np.repeat(np.arange(B), E)
+            res = {}
+            for mode in ("fp32", "plane", "records"):
+                eng = tmr_amd.TMREngine({k_: cuda(v) for k_, v in P.items()},
+                                        tmr_amd.PathConfig(emb_dim=emb, precision="bf16", decoder_kernel_size=k))
+                eng.xcorr_algo = "mfma"
+                eng.out_bf16 = mode != "fp32"
+                eng.out_records = mode == "records"
+                r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
+                assert eng.last_xcorr_out16 == (mode != "fp32")
+                res[mode] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
+            for mode in ("plane", "records"):
+                for a, b in zip(res["fp32"], res[mode]):
+                    assert bits_equal(a, b), (k, B, E, mode)
         # the module form (relu(f_TM) returned) keeps the fp32 plane
         eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
         assert not eng.last_xcorr_out16
@@ -1048,6 +1054,30 @@ def test_xcorr_split_launch_matches_single_kernel_launches():
         for t in range(3):
             assert bits_equal(res["split"][t][u], res[src][t][u]), (u, k, t)
     assert xcorr_unit_split(np.array([3, 15]), np.array([3, 15]), 3.0).tolist() == [False, True]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "f16"])
+@pytest.mark.parametrize("H,W,kmax", [(128, 128, 15), (96, 192, 31)])
+def test_xcorr_mfma_lds_fragments_bitexact(prec, H, W, kmax):
+    """The MFMA correlation with its A fragments built in-kernel from the
+    LDS-staged template (tmpl_split NULL, TMREngine.xcorr_afrag "lds") gives
+    the same f_TM, relu(f_TM) and per-unit max bit for bit as with the
+    pre-expanded fragments of tmr_template_split (3-term split; the one-term
+    precisions keep the pre-expanded fragments, so "lds" changes nothing)."""
+    C, B, E = 24, 2, 5
+    P = {k: cuda(v) for k, v in synth.reference_state_dict(41, cin=16, emb=C).items()}
+    fp = cuda(synth.normal(42 + W, (B, C, H, W)))
+    ex, _ = synth.exemplar_set(43 + kmax, B, E, H, W, 1, kmax)
+    boxes, ui = ex.reshape(-1, 4), np.repeat(np.arange(B), E)
+    res = {}
+    for af in ("split", "lds"):
+        eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C, precision=prec))
+        eng.xcorr_algo, eng.xcorr_afrag = "mfma", af
+        f, relu = eng.match(fp, ui, boxes, want_relu=True)
+        torch.cuda.synchronize()
+        res[af] = (f.float().cpu().numpy(), relu.float().cpu().numpy(), eng._memo_absmax(f, "ftm").cpu().numpy())
+    for t in range(3):
+        assert bits_equal(res["lds"][t], res["split"][t]), (prec, t)
 
 
 def test_nms_worst_case_dense_candidates():
