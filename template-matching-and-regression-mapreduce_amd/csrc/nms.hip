@@ -49,6 +49,7 @@ constexpr int CAP = 128;          // listed earlier-block suppressors per row
 
 struct BinHdr {
     float x0, y0, icx, icy, wmax, hmax;
+    float tq;  // the threshold the windows are narrowed by (0: overlap only)
     int gx, gy;
 };
 
@@ -176,13 +177,14 @@ __device__ __forceinline__ float box_area(float4 b) { return (b.z - b.x) * (b.w 
 // coordinate or a negative threshold gives one cell (every pair evaluated).
 __global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restrict__ cand_off, double thr,
                                                         NmsWork w) {
-    __shared__ float red[6][4];
+    __shared__ float red[8][4];
     __shared__ int bad[4];
     const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const float4 *sb = reinterpret_cast<const float4 *>(w.sb) + off;
-    float v[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, 0.0f, 0.0f};  // x1 min, y1 min, x1 max, y1 max, w, h
+    // x1 min, y1 min, x1 max, y1 max, w max, h max, w min, h min
+    float v[8] = {INFINITY, INFINITY, -INFINITY, -INFINITY, 0.0f, 0.0f, INFINITY, INFINITY};
     int nf = 0;
     for (int p = tid; p < n; p += 256) {
         const float4 bb = sb[p];
@@ -190,15 +192,17 @@ __global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restric
         v[0] = fminf(v[0], bb.x); v[1] = fminf(v[1], bb.y);
         v[2] = fmaxf(v[2], bb.x); v[3] = fmaxf(v[3], bb.y);
         v[4] = fmaxf(v[4], bb.z - bb.x); v[5] = fmaxf(v[5], bb.w - bb.y);
+        v[6] = fminf(v[6], bb.z - bb.x); v[7] = fminf(v[7], bb.w - bb.y);
     }
     for (int o = 32; o > 0; o >>= 1) {
         v[0] = fminf(v[0], __shfl_xor(v[0], o)); v[1] = fminf(v[1], __shfl_xor(v[1], o));
         v[2] = fmaxf(v[2], __shfl_xor(v[2], o)); v[3] = fmaxf(v[3], __shfl_xor(v[3], o));
         v[4] = fmaxf(v[4], __shfl_xor(v[4], o)); v[5] = fmaxf(v[5], __shfl_xor(v[5], o));
+        v[6] = fminf(v[6], __shfl_xor(v[6], o)); v[7] = fminf(v[7], __shfl_xor(v[7], o));
         nf |= __shfl_xor(nf, o);
     }
     if (lane == 0) {
-        for (int k = 0; k < 6; ++k) red[k][wv] = v[k];
+        for (int k = 0; k < 8; ++k) red[k][wv] = v[k];
         bad[wv] = nf;
     }
     __syncthreads();
@@ -207,6 +211,7 @@ __global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restric
         v[0] = fminf(v[0], red[0][q]); v[1] = fminf(v[1], red[1][q]);
         v[2] = fmaxf(v[2], red[2][q]); v[3] = fmaxf(v[3], red[3][q]);
         v[4] = fmaxf(v[4], red[4][q]); v[5] = fmaxf(v[5], red[5][q]);
+        v[6] = fminf(v[6], red[6][q]); v[7] = fminf(v[7], red[7][q]);
         nf |= bad[q];
     }
     BinHdr h;
@@ -214,6 +219,15 @@ __global__ __launch_bounds__(256) void bin_setup_kernel(const int64_t *__restric
     h.wmax = v[4]; h.hmax = v[5];
     h.gx = h.gy = 1;
     h.icx = h.icy = 0.0f;
+    // IoU > t needs |x1_i - x1_j| < (1 - t) max(w_i, w_j) and w_j < w_i / t
+    // (window()); that bound holds for the fp32 IoU too while no area or
+    // intersection can underflow or overflow to change the quotient by more
+    // than 2^-16 of t: box sides in [2^-60, 2^60], corners below 2^60 and
+    // t >= 2^-12.  Otherwise the windows bound overlap only (exact for fp32).
+    const bool narrow = thr >= 0x1p-12 && v[6] >= 0x1p-60f && v[7] >= 0x1p-60f && v[4] <= 0x1p60f &&
+                        v[5] <= 0x1p60f && fmaxf(fabsf(v[0]), fabsf(v[2])) <= 0x1p60f &&
+                        fmaxf(fabsf(v[1]), fabsf(v[3])) <= 0x1p60f;
+    h.tq = narrow ? (float)thr * (1.0f - 0x1p-16f) : 0.0f;
     if (!nf && thr >= 0.0 && n > 0) {
         const float rx = v[2] - v[0], ry = v[3] - v[1];
         const float mx = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[2])), 1e-30f);
@@ -286,62 +300,117 @@ __global__ __launch_bounds__(256) void bin_scan_kernel(NmsWork w) {
     if (tid == 255) cst[NCELL] = part[255];
 }
 
-// the cells a box's partners can lie in: corner windows
-// x1_j in (x1_i - wmax, x2_i), y1_j in (y1_i - hmax, y2_i), one cell of slack
+// the cells a box's partners can lie in: with t = hdr.tq,
+//   x1_j in (x1_i - f min(wmax, w_i / t), x1_i + f w_i),  f = 1 - t (+ 2^-16)
+// (IoU > t: the intersection is wider than t w_i and t w_j, so w_j < w_i / t
+// and |x1_i - x1_j| < (1 - t) max(w_i, w_j)); t = 0 is plain overlap,
+// x1_j in (x1_i - wmax, x2_i).  y likewise; one cell of slack each way.
+// Config E: 2680 -> 802 boxes per window at t = 0.5 (profiles/r05g dumps).
 __device__ __forceinline__ void window(const BinHdr &h, float4 bi, int &ax0, int &ax1, int &ay0, int &ay1) {
     if (h.gx == 1 && h.gy == 1) {
         ax0 = ax1 = ay0 = ay1 = 0;
         return;
     }
-    ax0 = max(cell_of(bi.x - h.wmax, h.x0, h.icx, h.gx) - 1, 0);
-    ax1 = min(cell_of(bi.z, h.x0, h.icx, h.gx) + 1, h.gx - 1);
-    ay0 = max(cell_of(bi.y - h.hmax, h.y0, h.icy, h.gy) - 1, 0);
-    ay1 = min(cell_of(bi.w, h.y0, h.icy, h.gy) + 1, h.gy - 1);
-    if (!(bi.z >= bi.x)) ax1 = h.gx - 1;  // inverted / NaN extents: the whole row of cells
-    if (!(bi.w >= bi.y)) ay1 = h.gy - 1;
+    const float f = (1.0f - h.tq) + 0x1p-16f;
+    const float bw = bi.z - bi.x, bh = bi.w - bi.y;
+    const float mw = h.tq > 0.0f ? fminf(h.wmax, bw / h.tq) : h.wmax;
+    const float mh = h.tq > 0.0f ? fminf(h.hmax, bh / h.tq) : h.hmax;
+    ax0 = max(cell_of(bi.x - f * mw, h.x0, h.icx, h.gx) - 1, 0);
+    ax1 = min(cell_of(bi.x + f * bw, h.x0, h.icx, h.gx) + 1, h.gx - 1);
+    ay0 = max(cell_of(bi.y - f * mh, h.y0, h.icy, h.gy) - 1, 0);
+    ay1 = min(cell_of(bi.y + f * bh, h.y0, h.icy, h.gy) + 1, h.gy - 1);
+    if (!(bw >= 0.0f)) { ax0 = 0; ax1 = h.gx - 1; }  // inverted / NaN extents: the whole row of cells
+    if (!(bh >= 0.0f)) { ay0 = 0; ay1 = h.gy - 1; }
 }
 
-// one thread per box of image blockIdx.y, taken in cell order
+__device__ __forceinline__ float rdl(float v, int q) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), q));
+}
+
+// One thread per box of image blockIdx.y, taken in cell order, and the
+// window scanned per WAVE: the 64 rows of a wave lie in a few neighbouring
+// cells of one grid row, so the wave walks the union of their windows once.
+// The entries of each window row come 64 at a time by one coalesced load
+// (lane l holds entry eb + l) and are broadcast by readlane, so the loads of
+// a batch are in flight together (one scalar load per entry had left the
+// kernel waiting on their latency: 2.9 ms at config E, profiles/r05f).  Every
+// lane tests each entry against its own row.  The lanes of a wave that spans
+// grid rows are taken one grid row at a time.
 __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ cand_off,
                                                     const int64_t *__restrict__ nb_off, double thr, NmsWork w) {
     const int g = blockIdx.y;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+    if (__builtin_amdgcn_readfirstlane(k) >= n) return;  // whole waves past the image
+    const int lane = threadIdx.x & 63;
+    const bool live = k < n;
     const BinHdr h = w.hdr[g];
     const bool prune = thr >= 0.0;
-    const int i = w.clist[off + k];
-    const float4 bi = reinterpret_cast<const float4 *>(w.sb)[off + i];
+    const int i = live ? w.clist[off + k] : 0;
+    const float4 bi = live ? reinterpret_cast<const float4 *>(w.sb)[off + i] : float4{0.0f, 0.0f, 0.0f, 0.0f};
     const float ai = box_area(bi);
     const int blk0 = i & ~63, blk1 = blk0 + 64;  // this row's 64-row block
-    const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
-    const int32_t *cl = w.clist + off;
-    const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
-    int32_t *lst = w.lst + (size_t)(nb_off[g] + (i >> 6)) * CAP * 64 + (i & 63);  // entry e at lst[e * 64]
+    const int32_t *__restrict__ cst = w.cst + (size_t)g * (NCELL + 1);
+    const int32_t *__restrict__ cl = w.clist + off;
+    const float4 *__restrict__ cb = reinterpret_cast<const float4 *>(w.cbox) + off;
+    // entry e of this row's list at lst[e * 64]
+    int32_t *__restrict__ lst = w.lst + (size_t)(nb_off[g] + (i >> 6)) * CAP * 64 + (i & 63);
     uint64_t diag = 0;
     int cnt = 0;
-    int ax0, ax1, ay0, ay1;
-    window(h, bi, ax0, ax1, ay0, ay1);
-    for (int ay = ay0; ay <= ay1; ++ay) {
-        const int e0 = cst[ay * h.gx + ax0], e1 = cst[ay * h.gx + ax1 + 1];  // the window row's cells are contiguous
-        for (int e = e0; e < e1; ++e) {
-            const int j = cl[e];
-            // earlier blocks: j may suppress i; later rows of this block: i may
-            // suppress j (the chain); the rest is the other row's business
-            if (j >= blk1 || (j >= blk0 && j <= i)) continue;
-            const float4 bj = cb[e];
-            if (!iou_over(bi, ai, bj, box_area(bj), thr, prune)) continue;
-            if (j > i) {
-                diag |= 1ull << (j & 63);
-            } else {
-                if (cnt < CAP) lst[cnt * 64] = j;
-                ++cnt;
+    int ax0 = 0, ax1 = -1, ay0 = 0, ay1 = -1;
+    if (live) window(h, bi, ax0, ax1, ay0, ay1);
+    // the grid row of each lane's own cell (the grouping key)
+    const int myrow = live ? cell_of(bi.y, h.y0, h.icy, h.gy) : -1;
+    uint64_t todo = __ballot(live);
+    while (todo) {
+        const int lead = __builtin_ctzll(todo);
+        const int grp = __shfl(myrow, lead);
+        const bool in = live && myrow == grp;
+        todo &= ~__ballot(in);
+        // the group's union window (wave-uniform)
+        int x0 = in ? ax0 : 1 << 30, x1 = in ? ax1 : -1, y0 = in ? ay0 : 1 << 30, y1 = in ? ay1 : -1;
+        for (int o = 32; o > 0; o >>= 1) {
+            x0 = min(x0, __shfl_xor(x0, o)); x1 = max(x1, __shfl_xor(x1, o));
+            y0 = min(y0, __shfl_xor(y0, o)); y1 = max(y1, __shfl_xor(y1, o));
+        }
+        x0 = __builtin_amdgcn_readfirstlane(x0); x1 = __builtin_amdgcn_readfirstlane(x1);
+        y0 = __builtin_amdgcn_readfirstlane(y0); y1 = __builtin_amdgcn_readfirstlane(y1);
+        for (int ay = y0; ay <= y1; ++ay) {
+            const bool rowin = in && ay >= ay0 && ay <= ay1;
+            if (!__ballot(rowin)) continue;
+            const int e0 = __builtin_amdgcn_readfirstlane(cst[ay * h.gx + x0]);
+            const int e1 = __builtin_amdgcn_readfirstlane(cst[ay * h.gx + x1 + 1]);
+            for (int eb = e0; eb < e1; eb += 64) {
+                const int el = eb + lane;
+                int jl = 0;
+                float4 bl = float4{0.0f, 0.0f, 0.0f, 0.0f};
+                if (el < e1) {
+                    jl = cl[el];
+                    bl = cb[el];
+                }
+                const int nq = min(64, e1 - eb);
+                for (int q = 0; q < nq; ++q) {  // wave-uniform entry
+                    const int j = __builtin_amdgcn_readlane(jl, q);
+                    const float4 bj = float4{rdl(bl.x, q), rdl(bl.y, q), rdl(bl.z, q), rdl(bl.w, q)};
+                    // earlier blocks: j may suppress i; later rows of this block: i may
+                    // suppress j (the chain); the rest is the other row's business
+                    if (!rowin || j >= blk1 || (j >= blk0 && j <= i)) continue;
+                    if (!iou_over(bi, ai, bj, box_area(bj), thr, prune)) continue;
+                    if (j > i) {
+                        diag |= 1ull << (j & 63);
+                    } else {
+                        if (cnt < CAP) lst[cnt * 64] = j;
+                        ++cnt;
+                    }
+                }
             }
         }
     }
-    w.diag[off + i] = diag;
-    w.lcnt[off + i] = cnt;
+    if (live) {
+        w.diag[off + i] = diag;
+        w.lcnt[off + i] = cnt;
+    }
 }
 
 // One wave per image: the greedy pass over the 64-row blocks in score order.
@@ -354,13 +423,26 @@ __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ 
 // listed ones kept, is settled by the wave rescanning its window (rare).
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
 constexpr int LBLK = CAP * 64;              // list entries per 64-row block
-constexpr int LDMA = LBLK * 4 / 1024;       // 1-KB DMA wave-instructions per block
 
-__device__ __forceinline__ void lists_dma(__amdgpu_buffer_rsrc_t r, int32_t *dst, int ib, int lane) {
-#pragma unroll 8
-    for (int q = 0; q < LDMA; ++q)
+// the first `rows` list entries of every row of block ib (4 entries of the
+// 64 rows per 1-KB DMA instruction)
+__device__ __forceinline__ void lists_dma(__amdgpu_buffer_rsrc_t r, int32_t *dst, int ib, int lane, int rows) {
+    const int nq = __builtin_amdgcn_readfirstlane((rows + 3) >> 2);
+    for (int q = 0; q < nq; ++q)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * 256), 16, lane * 16,
                                                  (uint32_t)ib * (LBLK * 4) + q * 1024, 0, 0);
+}
+
+// the wave's largest v in [0, CAP]: a bit at a time by ballots (no LDS
+// round trips, unlike a shuffle reduction)
+__device__ __forceinline__ int wave_max_cap(int v) {
+    int r = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const int c = r | (1 << b);
+        if (__ballot(v >= c)) r = c;
+    }
+    return r;
 }
 
 __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ cand_off,
@@ -374,6 +456,8 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
     int32_t *lbuf = reinterpret_cast<int32_t *>(keptb + w.lbuf_words);  // [2][LBLK], 16-B aligned
+    const int zw = (int)w.lbuf_words - 1;  // a word that stays zero (past the kept bitmap)
+    if (lane == 0) keptb[zw] = 0ull;
     const BinHdr h = w.hdr[g];
     const bool prune = thr >= 0.0;
     const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
@@ -382,29 +466,41 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
     const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(w.lst + (size_t)nb_off[g] * LBLK), (short)0, (int)((size_t)nb * LBLK * 4), 0x00020000);
     int cnt = 0;
+    // list lengths two blocks ahead (the DMA of block ib + 1 is sized by them)
     uint64_t diag = lane < n ? w.diag[off + lane] : 0ull;
     int lc = lane < n ? w.lcnt[off + lane] : 0;
-    lists_dma(lr, lbuf, 0, lane);
+    int lc1 = lane + 64 < n ? w.lcnt[off + 64 + lane] : 0;
+    lists_dma(lr, lbuf, 0, lane, wave_max_cap(min(lc, CAP)));
     for (int ib = 0; ib < nb; ++ib) {
         const int i = ib * 64 + lane;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block ib's lists (and registers) are in
         uint64_t dnext = 0ull;
-        int lnext = 0;
+        int lc2 = 0;
         if (ib + 1 < nb) {  // the next block, in flight meanwhile
-            lists_dma(lr, lbuf + ((ib + 1) & 1) * LBLK, ib + 1, lane);
-            if (i + 64 < n) {
-                dnext = w.diag[off + i + 64];
-                lnext = w.lcnt[off + i + 64];
-            }
+            lists_dma(lr, lbuf + ((ib + 1) & 1) * LBLK, ib + 1, lane, wave_max_cap(min(lc1, CAP)));
+            if (i + 64 < n) dnext = w.diag[off + i + 64];
+            if (i + 128 < n) lc2 = w.lcnt[off + i + 128];
         }
-        // removed by a kept earlier-block suppressor?
+        // removed by a kept earlier-block suppressor?  8 list entries per
+        // step, all 16 LDS reads unconditional so they are in flight together
+        // (entries past a row's count read stale buffer words, masked; a
+        // guarded read per entry had serialised them: 2.1 -> 3.4 ms, r05h)
         const int32_t *lb = lbuf + (ib & 1) * LBLK + lane;
         const int m = i < n ? min(lc, CAP) : 0;
-        bool rem = false;
-        for (int e = 0; e < m; ++e) {
-            const int j = lb[e * 64];
-            rem |= (keptb[j >> 6] >> (j & 63)) & 1ull;
+        // (e0 + 7 < CAP whenever e0 < m <= CAP; an entry past the count
+        // reads the always-zero word keptb[zw])
+        uint32_t rem32 = 0;
+        for (int e0 = 0; __ballot(!rem32 && e0 < m); e0 += 8) {
+            int jj[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) jj[t] = lb[(e0 + t) * 64];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int j = e0 + t < m ? jj[t] : zw * 64;
+                rem32 |= (uint32_t)(keptb[j >> 6] >> (j & 63)) & 1u;
+            }
         }
+        bool rem = rem32 != 0;
         // more suppressors than listed and none of the listed kept: rescan
         for (uint64_t ovf = __ballot(i < n && lc > CAP && !rem); ovf; ovf &= ovf - 1) {
             const int r = __builtin_ctzll(ovf);
@@ -451,7 +547,8 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
         cnt += __popcll(kept);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // keptb[ib] before the next block's reads
         diag = dnext;
-        lc = lnext;
+        lc = lc1;
+        lc1 = lc2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) kept_out[g] = cnt;
@@ -679,7 +776,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
                        nb_off, iou_threshold, w);
     TMR_CHECK_LAUNCH();
     // LDS: the kept bitmap (max_nb words, rounded to 16 B) + two list buffers
-    w.lbuf_words = (max_nb + 1) & ~int64_t(1);
+    w.lbuf_words = (max_nb + 2) & ~int64_t(1);  // + the zero word
     const size_t lds = sizeof(uint64_t) * (size_t)w.lbuf_words + 2 * sizeof(int32_t) * LBLK;
     TMR_REQUIRE(lds <= 160 * 1024);
     if (lds > 64 * 1024 && tmr_set_max_lds((const void *)greedy_kernel, lds) != hipSuccess) return TMR_E_HIP;

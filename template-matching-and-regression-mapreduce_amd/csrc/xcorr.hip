@@ -790,7 +790,7 @@ __device__ __forceinline__ void mfma_unit_lds(f32x4 (&acc)[NTW], const char *Fh,
 // OB: f_TM leaves as bf16 (the bf16 contract's detect path: the decoder's
 // bf16 records are bf16(f_TM) either way, so the fp32 plane is never needed;
 // half the bytes written here and read by the record pack)
-template <int NTW, int NV4, int TRB, int PM, bool OB = false, bool TL = false>
+template <int NTW, int NV4, int TRB, int PM, bool OB = false, bool TL = false, bool RC = false>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
@@ -948,7 +948,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                     r4[j] = (vy && xx >= pw && xx < pw + Wo) ? div_cr(acc[t][j] * inv, denom, rden) * sc : 0.0f;
                     vmax = fmaxf(vmax, fabsf(r4[j]));
                 }
-                if (OB && m.rks) {
+                if (RC) {
                     // the decoder's bf16 records directly (tmr_split_xpack16's layout: piece
                     // (c / 8) % 4 of chunk c / 32, element c % 8 of each pixel's 16 B): no
                     // f_TM plane, no record pass; the 8 channels of a piece come from 8
@@ -1045,14 +1045,22 @@ static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
     constexpr bool can_tl = PM == TMR_PREC_F16X3 && !OB;  // in-kernel fragments: 3-term only
     const bool tl = trows == nullptr;
     if (tl && !can_tl) return TMR_E_UNSUPPORTED;
-    const void *kfn = tl ? (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, can_tl>
-                         : (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false>;
+    // record output (OB only) and in-kernel fragments: instantiations of
+    // their own -- a runtime branch in the epilogue cost the plain bf16 plane
+    // launch 3.0 -> 3.7 ms at config C (registers), profiles/r05g
+    const bool rc = OB && m.rks != 0;
+    const void *kfn = tl   ? (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, can_tl>
+                      : rc ? (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false, OB>
+                           : (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false>;
     if (lds > 64 * 1024 &&
         tmr_set_max_lds(kfn, lds) != hipSuccess)
         return TMR_E_HIP;
     if (tl)
         hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, can_tl>), dim3(nblk), dim3(NT), lds, s, a, m,
                            trows, texp, a.out, a.units);
+    else if (rc)
+        hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false, OB>), dim3(nblk), dim3(NT), lds, s, a,
+                           m, trows, texp, a.out, a.units);
     else
         hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false>), dim3(nblk), dim3(NT), lds, s, a, m,
                            trows, texp, a.out, a.units);

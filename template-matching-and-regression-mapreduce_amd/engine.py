@@ -610,8 +610,11 @@ class TMREngine:
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
         self.last_xcorr_out16 = False
-        # ... and as the decoder's records themselves (no plane, no record pass)
-        self.out_records = True
+        # ... or as the decoder's records themselves (no plane, no record pass):
+        # off by default -- each block is one channel, so a record's 16 B come
+        # from 8 blocks as 2-B stores: config C correlation 3.7 -> 8.0 ms, step
+        # 53.3 -> 56.7 ms against the plane + record pass (profiles/r05g)
+        self.out_records = os.environ.get("TMR_XCORR_RECORDS", "0") == "1"
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False

@@ -709,6 +709,60 @@ def test_nms_binned_edge_cases_vs_oracle(thr):
         assert bits_equal(L[k].cpu().numpy()[:, 0], sc[keep]), (thr, k)
 
 
+def _nms_threshold_cases():
+    """Images for the threshold-narrowed windows (nms.hip window(): IoU > t
+    bounds the corner offset by (1 - t) max(w_i, w_j) and w_j by w_i / t):
+    box pairs shifted to IoU = t within a few ulps either side, nested
+    boxes at area ratio ~ t, sizes spread over 1000x in one image, identical
+    and near-identical boxes, very small and very large boxes."""
+    r = np.random.default_rng(91)
+    cases = []
+    for t in (0.3, 0.5, 0.7, 0.99):
+        n = 300
+        xy = (r.random((n, 2)) * 0.8).astype(np.float32)
+        sd = (0.01 + r.random((n, 1)) * 0.1).astype(np.float32)
+        a = np.concatenate([xy, xy + sd], 1).astype(np.float32)
+        d = sd[:, 0] * np.float32((1 - t) / (1 + t))  # IoU((s - d) / (s + d)) = t
+        d = np.nextafter(d, np.where(r.random(n) < 0.5, 0, 1).astype(np.float32))
+        bsh = a.copy()
+        bsh[:, 0] += d
+        bsh[:, 2] += d
+        k = r.integers(0, 2, n)  # or shifted left / up
+        bsh[k == 1] = a[k == 1] - np.stack([d * 0, d, d * 0, d], 1)[k == 1]
+        cases.append(np.concatenate([a, bsh]).astype(np.float32))
+    xy = r.random((900, 2), np.float32) * 0.7
+    side = (10.0 ** r.uniform(-3.5, -0.5, (900, 1))).astype(np.float32)
+    nest = np.concatenate([xy, xy + side], 1).astype(np.float32)
+    inner = nest[::2].copy()
+    f = np.sqrt(r.uniform(0.2, 0.9, (inner.shape[0], 1))).astype(np.float32)
+    inner[:, 2:] = inner[:, :2] + (inner[:, 2:] - inner[:, :2]) * f
+    cases.append(np.concatenate([nest, inner, nest[:50]]).astype(np.float32))  # + exact duplicates
+    xy = r.random((600, 2), np.float32) * 1e-15
+    cases.append(np.concatenate([xy, xy + 1e-17 + r.random((600, 2), np.float32) * 3e-16], 1).astype(np.float32))
+    xy = r.random((600, 2), np.float32) * 1e20
+    cases.append(np.concatenate([xy, xy + 1e18 + r.random((600, 2), np.float32) * 3e19], 1).astype(np.float32))
+    out = []
+    for bx in cases:
+        sc = (np.round(r.random(len(bx)) * 64) / 64).astype(np.float32)
+        out.append((bx, sc))
+    return out
+
+
+@pytest.mark.parametrize("thr", [1e-4, 3e-4, 0.3, 0.5, 0.7, 0.99, 1.0, 1.5])
+def test_nms_threshold_windows_vs_oracle(thr):
+    """The windows narrowed by the threshold miss no suppressing pair: keep
+    lists bit-exact vs the oracle on boundary pairs (IoU = t +- ulps), nested
+    boxes, 1000x size spreads, duplicates, tiny and huge boxes, thresholds
+    below the narrowing cut-off (2^-12) and at / above 1."""
+    cases = _nms_threshold_cases()
+    L, Bx, R = tmr_amd.NMS([cuda(np.stack([sc, np.zeros_like(sc)], 1)) for bx, sc in cases],
+                           [cuda(bx) for bx, sc in cases], [cuda(bx[:, :2].copy()) for bx, sc in cases], thr)
+    for k, (bx, sc) in enumerate(cases):
+        keep = oracle.nms(bx, sc, thr)
+        assert bits_equal(Bx[k].cpu().numpy(), bx[keep]), (thr, k, len(keep), Bx[k].shape[0])
+        assert bits_equal(L[k].cpu().numpy()[:, 0], sc[keep]), (thr, k)
+
+
 def test_nms_binned_nonfinite_boxes_match_dense():
     """Non-finite box coordinates put the image in one bin (every pair
     evaluated with the kernels' own fmaxf/fminf arithmetic): an image of
