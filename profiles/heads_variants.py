@@ -18,6 +18,8 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   imgmajor an image's 3 units innermost in the heads grid (acc0 tile reuse; a correct build
            for 3 units per image)
+  gnolist / gnochain / gnorescan   the NMS greedy wave without its list test / its
+           in-block chain / its overflow rescan (wrong keep lists; greedy_kernel time only)
   l2dma    every DMA re-reads the first chunk's halo / first step's weights:
            the same instruction stream with real operand data, but L2-resident
            (no MALL / HBM traffic)
@@ -111,10 +113,20 @@ def variant_source(name: str, src: str) -> str:
             u = L / per_unit;
             r = L - u * per_unit;
         }""")
+    if name == "gnolist":
+        return _sub(src, "        bool rem = rem32 != 0;", "        bool rem = false; (void)rem32;")
+    if name == "gnochain":
+        return _sub(src, "        for (uint64_t avail = ~word; avail;) {  // the surviving rows, lowest first",
+                    "        kept = ~word; (void)dlo; (void)dhi;\n        for (uint64_t avail = 0; avail;) {")
+    if name == "gnorescan":
+        return _sub(src, "        for (uint64_t ovf = __ballot(i < n && lc > CAP && !rem); ovf; ovf &= ovf - 1) {",
+                    "        for (uint64_t ovf = 0; ovf; ovf &= ovf - 1) {")
     raise SystemExit(f"unknown variant {name}")
 
 
 def variant_file(name: str) -> str:
+    if name.startswith("g"):
+        return "nms.hip"
     return "xcorr.hip" if name.startswith(("tsparse", "xl2band", "xl2a")) else "conv_split.hip"
 
 

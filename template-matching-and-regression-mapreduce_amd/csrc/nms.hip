@@ -7,9 +7,12 @@
 //
 //   gather : union per image in unit order (dummy row for an empty unit)
 //            + the local index of every row
-//   sort   : rocprim segmented radix sort of (score, index) pairs, descending
-//            and stable: ties keep the lower index first, as torchvision's
-//            stable sort (O(n log) per image instead of O(n^2) rank counting)
+//   sort   : ONE device-wide rocprim radix sort of (image, score) keys --
+//            the image in the high bits, the score's descending radix key
+//            below -- with the local index as value: stable, so ties keep the
+//            lower index first, as torchvision's stable sort (a segmented
+//            sort of a few large images ran a workgroup per image: 0.75 ms
+//            at config E)
 //   bins   : the sorted boxes are binned by their top-left corner on a
 //            per-image grid (<= 64 x 64 cells); two boxes can only overlap
 //            (and so only suppress, for iou_threshold >= 0) when each one's
@@ -35,7 +38,7 @@
 // Built with -ffp-contract=off.
 #include <algorithm>
 
-#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "tmr_common.h"
 
@@ -45,7 +48,9 @@ namespace {
 constexpr int64_t SORT_SLACK = 1 << 20;
 constexpr int GB = 64;            // bins per axis (at most)
 constexpr int NCELL = GB * GB;
-constexpr int CAP = 128;          // listed earlier-block suppressors per row
+constexpr int CAP = 128;          // listed earlier-block suppressors per row (config E: p99 68, max ~100;
+                                  // at 96 the overflow rescans cost 0.24 ms of 1.42, profiles/r05m)
+constexpr int LUNR = 32;          // list entries tested per step of the greedy (CAP % LUNR == 0)
 
 struct BinHdr {
     float x0, y0, icx, icy, wmax, hmax;
@@ -55,7 +60,8 @@ struct BinHdr {
 
 struct NmsWork {
     float *s;        // [T] scores (unit order)
-    float *skeys;    // [T] sorted scores (unused beyond the sort)
+    uint64_t *key;   // [T] (image << 32) | descending score key
+    uint64_t *skey;  // [T] sorted keys (unused beyond the sort)
     float *b;        // [T][4]
     float *r;        // [T][2]
     int32_t *idx;    // [T] local row index (sort values in)
@@ -68,6 +74,8 @@ struct NmsWork {
     float *cbox;     // [T][4] their boxes
     uint64_t *diag;  // [T] in-block suppression word of each sorted row (later rows it suppresses)
     int32_t *lcnt;   // [T] earlier-block suppressors of each sorted row
+    uint64_t *keptw; // [sum_nb] kept word of each 64-row block
+    int32_t *kbase;  // [sum_nb] kept rows before each block
     int32_t *lst;    // [sum_nb][CAP][64] the first CAP of them found (sorted positions),
                      // per 64-row block entry-major: entry e of row i at
                      // ((nb_off[g] + i/64) * CAP + e) * 64 + i%64
@@ -78,13 +86,16 @@ struct NmsWork {
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-inline int64_t sort_temp_bound(int64_t T, int G) { return 8 * T + SORT_SLACK + 64 * (int64_t)(G + 1); }
+// rocprim's radix sort keeps its own key + value double buffers in the
+// temporary storage (12 B per candidate) beside its histograms
+inline int64_t sort_temp_bound(int64_t T, int G) { return 16 * T + SORT_SLACK + 64 * (int64_t)(G + 1); }
 
 inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int G) {
     NmsWork w;
     char *p = (char *)work;
     w.s = (float *)p; p += align256(sizeof(float) * T);
-    w.skeys = (float *)p; p += align256(sizeof(float) * T);
+    w.key = (uint64_t *)p; p += align256(sizeof(uint64_t) * T);
+    w.skey = (uint64_t *)p; p += align256(sizeof(uint64_t) * T);
     w.b = (float *)p; p += align256(sizeof(float) * 4 * T);
     w.r = (float *)p; p += align256(sizeof(float) * 2 * T);
     w.idx = (int32_t *)p; p += align256(sizeof(int32_t) * T);
@@ -97,6 +108,8 @@ inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int G) {
     w.cbox = (float *)p; p += align256(sizeof(float) * 4 * T);
     w.diag = (uint64_t *)p; p += align256(sizeof(uint64_t) * T);
     w.lcnt = (int32_t *)p; p += align256(sizeof(int32_t) * T);
+    w.keptw = (uint64_t *)p; p += align256(sizeof(uint64_t) * sum_nb);
+    w.kbase = (int32_t *)p; p += align256(sizeof(int32_t) * sum_nb);
     w.lst = (int32_t *)p; p += align256(sizeof(int32_t) * CAP * 64 * sum_nb);
     w.temp = p;
     w.temp_bytes = sort_temp_bound(T, G);
@@ -106,6 +119,18 @@ inline NmsWork carve(void *work, int64_t T, int64_t sum_nb, int G) {
 inline int64_t work_bytes(int64_t T, int64_t sum_nb, int G) {
     const NmsWork w = carve(nullptr, T, sum_nb, G);
     return (int64_t)(w.temp - (char *)nullptr) + w.temp_bytes + 256;
+}
+
+__device__ __forceinline__ uint32_t radix_key(float f) {
+    uint32_t b = __float_as_uint(f);
+    if (b == 0x80000000u) b = 0u;  // rocprim's digit extractor: -0.0 sorts as +0.0
+    return b ^ ((b & 0x80000000u) ? 0xffffffffu : 0x80000000u);
+}
+
+// the sort key of candidate (image g, score f): images ascending, scores
+// descending in rocprim's float key order
+__device__ __forceinline__ uint64_t sort_key(int g, float f) {
+    return ((uint64_t)(uint32_t)g << 32) | (uint64_t)(~radix_key(f));
 }
 
 __global__ void gather_kernel(const float *__restrict__ logits, const float *__restrict__ box,
@@ -121,6 +146,7 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
         if (n == 0) {
             if (threadIdx.x == 0) {
                 w.s[pos] = 0.0f;
+                w.key[pos] = sort_key(g, 0.0f);
                 w.b[4 * pos + 0] = 0.0f; w.b[4 * pos + 1] = 0.0f;
                 w.b[4 * pos + 2] = 1e-14f; w.b[4 * pos + 3] = 1e-14f;
                 w.r[2 * pos + 0] = 0.0f; w.r[2 * pos + 1] = 0.0f;
@@ -131,7 +157,9 @@ __global__ void gather_kernel(const float *__restrict__ logits, const float *__r
         }
         const size_t src = (size_t)unit_off[u];
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            w.s[pos + i] = logits[2 * (src + i)];
+            const float sc = logits[2 * (src + i)];
+            w.s[pos + i] = sc;
+            w.key[pos + i] = sort_key(g, sc);
             const float4 bb = reinterpret_cast<const float4 *>(box)[src + i];
             reinterpret_cast<float4 *>(w.b)[pos + i] = bb;
             w.r[2 * (pos + i) + 0] = ref[2 * (src + i) + 0];
@@ -417,87 +445,87 @@ __global__ __launch_bounds__(256) void pairs_kernel(const int64_t *__restrict__ 
 // A row is removed when one of its earlier-block suppressors was kept (a
 // bitmap of the kept rows in LDS; each lane tests its own row's list, LDS
 // reads, no scatter), then the block's chain is resolved from the diagonal
-// words in registers.  A block's lists (CAP x 64 entries, entry-major, so
-// lane r reads column r conflict free) arrive in LDS by buffer-to-LDS DMA one
-// block ahead.  A row with more than CAP earlier suppressors, none of its
-// listed ones kept, is settled by the wave rescanning its window (rare).
+// words.  A block's lists (CAP x 64 entries, entry-major, so lane r reads
+// column r conflict free), diagonal words and list counts arrive in LDS by
+// buffer-to-LDS DMA GP blocks ahead into GP slots, so the wave's serial path
+// waits on no memory latency (the kept rows, once written inside the loop,
+// put two dependent global loads on every block: 1.83 -> 1.58 ms at config
+// E without them; a third block of look-ahead measured 1.58 -> 1.46).  The DMA count per block is fixed, so one
+// s_waitcnt vmcnt(N) waits for exactly the block about to be read.  A row
+// with more than CAP earlier suppressors, none of its listed ones kept, is
+// settled by the wave rescanning its window (rare).
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
-constexpr int LBLK = CAP * 64;              // list entries per 64-row block
+constexpr int LBLK = CAP * 64;                  // list entries per 64-row block
+constexpr int GP = 2;                           // look-ahead (blocks) = slots
+constexpr int SLOT_W = LBLK + 128 + 64;         // int32 words per slot: lists, 64 diag words, 64 counts
+constexpr int DMA_PER_BLOCK = CAP / 4 + 3;      // 1-KB list pieces + 2 diag + 1 count instructions
+static_assert(CAP % LUNR == 0 && CAP % 4 == 0, "list steps and 1-KB DMA pieces");
+static_assert((GP - 1) * DMA_PER_BLOCK <= 63, "vmcnt range");
 
-// the first `rows` list entries of every row of block ib (4 entries of the
-// 64 rows per 1-KB DMA instruction)
-__device__ __forceinline__ void lists_dma(__amdgpu_buffer_rsrc_t r, int32_t *dst, int ib, int lane, int rows) {
-    const int nq = __builtin_amdgcn_readfirstlane((rows + 3) >> 2);
-    for (int q = 0; q < nq; ++q)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * 256), 16, lane * 16,
-                                                 (uint32_t)ib * (LBLK * 4) + q * 1024, 0, 0);
-}
-
-// the wave's largest v in [0, CAP]: a bit at a time by ballots (no LDS
-// round trips, unlike a shuffle reduction)
-__device__ __forceinline__ int wave_max_cap(int v) {
-    int r = 0;
+__device__ __forceinline__ void block_dma(__amdgpu_buffer_rsrc_t rl, __amdgpu_buffer_rsrc_t rd,
+                                          __amdgpu_buffer_rsrc_t rc, int32_t *slot, int ib, int lane) {
 #pragma unroll
-    for (int b = 7; b >= 0; --b) {
-        const int c = r | (1 << b);
-        if (__ballot(v >= c)) r = c;
-    }
-    return r;
+    for (int q = 0; q < CAP / 4; ++q)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_ptr_t)(slot + q * 256), 16, lane * 16,
+                                                 (uint32_t)ib * (LBLK * 4) + q * 1024, 0, 0);
+    // rows past the image read out of range: zero (and masked anyway)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_ptr_t)(slot + LBLK), 4, lane * 4, (uint32_t)ib * 512, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_ptr_t)(slot + LBLK + 64), 4, lane * 4,
+                                             (uint32_t)ib * 512 + 256, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lds_ptr_t)(slot + LBLK + 128), 4, lane * 4, (uint32_t)ib * 256, 0,
+                                             0);
 }
 
 __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ cand_off,
                                                     const int64_t *__restrict__ nb_off, double thr, NmsWork w,
-                                                    float *__restrict__ out_logits, float *__restrict__ out_boxes,
-                                                    float *__restrict__ out_refs, int64_t *__restrict__ out_keep,
                                                     int32_t *__restrict__ kept_out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long keptb[];  // [nb], then 2 list buffers
+    extern __shared__ __attribute__((aligned(16))) unsigned long long keptb[];  // [lbuf_words], then GP slots
     const int g = blockIdx.x, lane = threadIdx.x;
     const int64_t off = cand_off[g];
     const int n = (int)(cand_off[g + 1] - off);
     const int nb = (n + 63) / 64;
-    int32_t *lbuf = reinterpret_cast<int32_t *>(keptb + w.lbuf_words);  // [2][LBLK], 16-B aligned
+    int32_t *slots = reinterpret_cast<int32_t *>(keptb + w.lbuf_words);  // [GP][SLOT_W], 16-B aligned
     const int zw = (int)w.lbuf_words - 1;  // a word that stays zero (past the kept bitmap)
+    const uint32_t *kept32 = reinterpret_cast<const uint32_t *>(keptb);
     if (lane == 0) keptb[zw] = 0ull;
     const BinHdr h = w.hdr[g];
     const bool prune = thr >= 0.0;
     const int32_t *cst = w.cst + (size_t)g * (NCELL + 1);
     const int32_t *cl = w.clist + off;
     const float4 *cb = reinterpret_cast<const float4 *>(w.cbox) + off;
-    const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(w.lst + (size_t)nb_off[g] * LBLK), (short)0, (int)((size_t)nb * LBLK * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(w.diag + off), (short)0, (int)((size_t)n * 8), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(w.lcnt + off), (short)0, (int)((size_t)n * 4), 0x00020000);
     int cnt = 0;
-    // list lengths two blocks ahead (the DMA of block ib + 1 is sized by them)
-    uint64_t diag = lane < n ? w.diag[off + lane] : 0ull;
-    int lc = lane < n ? w.lcnt[off + lane] : 0;
-    int lc1 = lane + 64 < n ? w.lcnt[off + 64 + lane] : 0;
-    lists_dma(lr, lbuf, 0, lane, wave_max_cap(min(lc, CAP)));
+    for (int q = 0; q < GP && q < nb; ++q) block_dma(rl, rd, rc, slots + q * SLOT_W, q, lane);
     for (int ib = 0; ib < nb; ++ib) {
         const int i = ib * 64 + lane;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block ib's lists (and registers) are in
-        uint64_t dnext = 0ull;
-        int lc2 = 0;
-        if (ib + 1 < nb) {  // the next block, in flight meanwhile
-            lists_dma(lr, lbuf + ((ib + 1) & 1) * LBLK, ib + 1, lane, wave_max_cap(min(lc1, CAP)));
-            if (i + 64 < n) dnext = w.diag[off + i + 64];
-            if (i + 128 < n) lc2 = w.lcnt[off + i + 128];
-        }
-        // removed by a kept earlier-block suppressor?  8 list entries per
-        // step, all 16 LDS reads unconditional so they are in flight together
-        // (entries past a row's count read stale buffer words, masked; a
-        // guarded read per entry had serialised them: 2.1 -> 3.4 ms, r05h)
-        const int32_t *lb = lbuf + (ib & 1) * LBLK + lane;
-        const int m = i < n ? min(lc, CAP) : 0;
-        // (e0 + 7 < CAP whenever e0 < m <= CAP; an entry past the count
+        // block ib's DMA is done once at most the later blocks' are in flight
+        if (ib + GP <= nb)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((GP - 1) * DMA_PER_BLOCK) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int32_t *slot = slots + (ib % GP) * SLOT_W;
+        const uint64_t diag = i < n ? reinterpret_cast<const uint64_t *>(slot + LBLK)[lane] : 0ull;
+        const int lc = i < n ? slot[LBLK + 128 + lane] : 0;
+        // removed by a kept earlier-block suppressor?  LUNR list entries per
+        // step, all LDS reads unconditional so they are in flight together
+        // (e0 + LUNR <= CAP whenever e0 < m <= CAP; an entry past the count
         // reads the always-zero word keptb[zw])
+        const int32_t *lb = slot + lane;
+        const int m = min(lc, CAP);
         uint32_t rem32 = 0;
-        for (int e0 = 0; __ballot(!rem32 && e0 < m); e0 += 8) {
-            int jj[8];
+        for (int e0 = 0; __ballot(!rem32 && e0 < m); e0 += LUNR) {
+            int jj[LUNR];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) jj[t] = lb[(e0 + t) * 64];
+            for (int t = 0; t < LUNR; ++t) jj[t] = lb[(e0 + t) * 64];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
+            for (int t = 0; t < LUNR; ++t) {
                 const int j = e0 + t < m ? jj[t] : zw * 64;
-                rem32 |= (uint32_t)(keptb[j >> 6] >> (j & 63)) & 1u;
+                rem32 |= (kept32[j >> 5] >> (j & 31)) & 1u;  // 32-bit halves: 4-B reads
             }
         }
         bool rem = rem32 != 0;
@@ -533,25 +561,72 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
             avail = bit == 63 ? 0ull : ~word & (~0ull << (bit + 1));
         }
         if (lane == 0) keptb[ib] = kept;
-        if ((kept >> lane) & 1ull) {
-            const int pos = cnt + __popcll(kept & ((1ull << lane) - 1));
-            const int li = min(max(w.order[off + i], 0), n - 1);
-            const int64_t src = off + li, dst = off + pos;
-            out_logits[2 * dst + 0] = w.s[src];
-            out_logits[2 * dst + 1] = 0.0f;
-            reinterpret_cast<float4 *>(out_boxes)[dst] = reinterpret_cast<const float4 *>(w.b)[src];
-            out_refs[2 * dst + 0] = w.r[2 * src + 0];
-            out_refs[2 * dst + 1] = w.r[2 * src + 1];
-            if (out_keep) out_keep[dst] = li;
-        }
         cnt += __popcll(kept);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // keptb[ib] before the next block's reads
-        diag = dnext;
-        lc = lc1;
-        lc1 = lc2;
+        // keptb[ib] before the next block's reads; this slot's reads before
+        // the DMA that refills it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (ib + GP < nb) block_dma(rl, rd, rc, slot, ib + GP, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int q = lane; q < nb; q += 64) w.keptw[nb_off[g] + q] = keptb[q];
     if (lane == 0) kept_out[g] = cnt;
+}
+
+// kept rows before each 64-row block (exclusive scan of the kept words'
+// popcounts), one workgroup per image
+__global__ __launch_bounds__(256) void kept_scan_kernel(const int64_t *__restrict__ cand_off,
+                                                        const int64_t *__restrict__ nb_off, NmsWork w) {
+    __shared__ int part[256];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int n = (int)(cand_off[g + 1] - cand_off[g]);
+    const int nb = (n + 63) / 64;
+    const int per = (nb + 255) / 256, q0 = min(tid * per, nb), q1 = min(q0 + per, nb);
+    const uint64_t *kw = w.keptw + nb_off[g];
+    int32_t *kb = w.kbase + nb_off[g];
+    int sum = 0;
+    for (int q = q0; q < q1; ++q) sum += __popcll(kw[q]);
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int t = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += t;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;
+    for (int q = q0; q < q1; ++q) {
+        kb[q] = run;
+        run += __popcll(kw[q]);
+    }
+}
+
+// The kept rows out, chip-wide: one thread per sorted row, its slot from the
+// block's kept word and running count (greedy_kernel).  Writing them inside
+// the greedy wave had put two dependent global loads (order, then the row)
+// on every block's serial path.
+__global__ __launch_bounds__(256) void emit_kernel(const int64_t *__restrict__ cand_off,
+                                                   const int64_t *__restrict__ nb_off, NmsWork w,
+                                                   float *__restrict__ out_logits, float *__restrict__ out_boxes,
+                                                   float *__restrict__ out_refs, int64_t *__restrict__ out_keep) {
+    const int g = blockIdx.y;
+    const int64_t off = cand_off[g];
+    const int n = (int)(cand_off[g + 1] - off);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int64_t wb = nb_off[g] + (p >> 6);
+    const uint64_t kept = w.keptw[wb];
+    const int lane = p & 63;
+    if (!((kept >> lane) & 1ull)) return;
+    const int pos = w.kbase[wb] + __popcll(kept & ((1ull << lane) - 1));
+    const int li = min(max(w.order[off + p], 0), n - 1);
+    const int64_t src = off + li, dst = off + pos;
+    out_logits[2 * dst + 0] = w.s[src];
+    out_logits[2 * dst + 1] = 0.0f;
+    reinterpret_cast<float4 *>(out_boxes)[dst] = reinterpret_cast<const float4 *>(w.b)[src];
+    out_refs[2 * dst + 0] = w.r[2 * src + 0];
+    out_refs[2 * dst + 1] = w.r[2 * src + 1];
+    if (out_keep) out_keep[dst] = li;
 }
 
 // Calls whose every image has at most SMALL_N candidates (the module API's
@@ -563,11 +638,6 @@ __global__ __launch_bounds__(64) void greedy_kernel(const int64_t *__restrict__ 
 // + strips, no work buffer.  Same keep lists by construction.
 constexpr int SMALL_N = TMR_NMS_SMALL;
 
-__device__ __forceinline__ uint32_t radix_key(float f) {
-    uint32_t b = __float_as_uint(f);
-    if (b == 0x80000000u) b = 0u;  // rocprim's digit extractor: -0.0 sorts as +0.0
-    return b ^ ((b & 0x80000000u) ? 0xffffffffu : 0x80000000u);
-}
 
 // one image's union (units u_beg..u_end-1, n <= SMALL_N rows) -> kept rows at
 // out[off ...], kept_out[g]; one workgroup of SMALL_N threads
@@ -738,7 +808,7 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     TMR_REQUIRE(total_cand < (1ll << 31));
     const int64_t max_nb = (max_cand + 63) / 64;
     TMR_REQUIRE(max_nb < (1 << 20) && G < 65536);
-    TMR_REQUIRE(max_nb * 8 <= 90 * 1024);  // the kept bitmap in LDS (beside 64 KB of list buffers)
+    TMR_REQUIRE(max_nb * 8 <= 80 * 1024);  // the kept bitmap in LDS (beside ~66 KB of list slots)
     hipStream_t s = tmr_stream(stream);
     if (max_cand <= SMALL_N) {  // every image fits one workgroup
         hipLaunchKernelGGL(nms_small_kernel, dim3(G), dim3(SMALL_N), 0, s, logits, box, ref, counts, unit_off,
@@ -751,14 +821,15 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
                        seg_units, cand_off, w);
     TMR_CHECK_LAUNCH();
     size_t tb = 0;
-    if (rocprim::segmented_radix_sort_pairs_desc(nullptr, tb, w.s, w.skeys, w.idx, w.order,
-                                                 (unsigned)total_cand, (unsigned)G, cand_off, cand_off + 1,
-                                                 0, 32, s) != hipSuccess)
+    int gbits = 0;
+    while ((1 << gbits) < G) ++gbits;
+    const unsigned end_bit = 32u + (unsigned)gbits;  // the image bits only as far as G needs
+    if (rocprim::radix_sort_pairs(nullptr, tb, w.key, w.skey, w.idx, w.order, (unsigned)total_cand, 0u, end_bit,
+                                  s) != hipSuccess)
         return TMR_E_HIP;
     if ((int64_t)tb > w.temp_bytes) return TMR_E_INVALID;
-    if (rocprim::segmented_radix_sort_pairs_desc(w.temp, tb, w.s, w.skeys, w.idx, w.order,
-                                                 (unsigned)total_cand, (unsigned)G, cand_off, cand_off + 1,
-                                                 0, 32, s) != hipSuccess)
+    if (rocprim::radix_sort_pairs(w.temp, tb, w.key, w.skey, w.idx, w.order, (unsigned)total_cand, 0u, end_bit,
+                                  s) != hipSuccess)
         return TMR_E_HIP;
     const dim3 per_box((unsigned)std::min<int64_t>(tmr_cdiv(max_cand, 256), 1024), G);
     hipLaunchKernelGGL(sort_boxes_kernel, per_box, dim3(256), 0, s, cand_off, G, w);
@@ -775,13 +846,17 @@ extern "C" int tmr_nms(const float *logits, const float *box, const float *ref,
     hipLaunchKernelGGL(pairs_kernel, dim3((unsigned)tmr_cdiv(max_cand, 256), G), dim3(256), 0, s, cand_off,
                        nb_off, iou_threshold, w);
     TMR_CHECK_LAUNCH();
-    // LDS: the kept bitmap (max_nb words, rounded to 16 B) + two list buffers
-    w.lbuf_words = (max_nb + 2) & ~int64_t(1);  // + the zero word
-    const size_t lds = sizeof(uint64_t) * (size_t)w.lbuf_words + 2 * sizeof(int32_t) * LBLK;
+    // LDS: the kept bitmap (max_nb words + the zero word, rounded to 16 B) + GP slots
+    w.lbuf_words = (max_nb + 2) & ~int64_t(1);
+    const size_t lds = sizeof(uint64_t) * (size_t)w.lbuf_words + GP * sizeof(int32_t) * SLOT_W;
     TMR_REQUIRE(lds <= 160 * 1024);
     if (lds > 64 * 1024 && tmr_set_max_lds((const void *)greedy_kernel, lds) != hipSuccess) return TMR_E_HIP;
-    hipLaunchKernelGGL(greedy_kernel, dim3(G), dim3(64), lds, s, cand_off, nb_off, iou_threshold, w, out_logits,
-                       out_boxes, out_refs, out_keep, kept);
+    hipLaunchKernelGGL(greedy_kernel, dim3(G), dim3(64), lds, s, cand_off, nb_off, iou_threshold, w, kept);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(kept_scan_kernel, dim3(G), dim3(256), 0, s, cand_off, nb_off, w);
+    TMR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(emit_kernel, dim3((unsigned)tmr_cdiv(max_cand, 256), G), dim3(256), 0, s, cand_off, nb_off,
+                       w, out_logits, out_boxes, out_refs, out_keep);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
