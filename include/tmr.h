@@ -319,7 +319,8 @@ int tmr_maxpool3x3(const float *x, int64_t planes, int H, int W, int mask9, floa
  * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u]; a unit
  * with no peak (counts[u] = 0) gets the reference's dummy row at its row 0
  * (logits (0,0), box (0,0,1e-14,1e-14), ref (0,0); TM_utils.py:288-291).
- * prob [U,H,W] receives the probability map (required).
+ * prob [U,H,W] receives the probability map, or NULL: not written (and the
+ * sigmoid of pixels whose logit lies well below the threshold is skipped).
  * exp_table (device, nullable): the reference-exp table (tmr_amd/exp_table.py:
  * 128-B header, uint32 offsets[65537], sorted uint16 low halves).  The decode's
  * exp (TM_utils.py:272) is the correctly rounded value except at the table's

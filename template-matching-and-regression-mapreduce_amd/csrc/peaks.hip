@@ -71,16 +71,19 @@ __global__ void maxpool3x3_kernel(const float *__restrict__ x, int64_t n, int H,
 // the unit's map is walked in chunks of R whole rows; each chunk and its two
 // halo rows (zero outside the image: F.unfold's padding) are staged in LDS as
 // probabilities (sigmoid computed once per staged element, the chunk's own
-// rows also written to `prob`).  Then every wave takes 64 consecutive
-// row-major pixels per step: is_peak from LDS, a 64-bit ballot, mbcnt for the
-// lane's in-order slot, and a workgroup scan of the waves' popcounts for the
-// wave's base -- so the candidates leave in row-major (torch.where) order in
-// ONE pass, decoded in place.  Round 4's kernel gave each thread a contiguous
-// run of pixels (lanes strided by that run: uncoalesced loads) and evaluated
-// the 9-tap test twice (count pass, write pass).
+// rows also written to `prob` when asked).  Every wave takes 64 consecutive
+// row-major pixels per step and keeps the step's is_peak ballot in LDS; after
+// ONE barrier every lane finds its slot from the ballots of the steps and
+// waves before it (+ mbcnt), so the candidates leave in row-major
+// (torch.where) order, three barriers per chunk (round 5's first ballot
+// kernel synchronised twice per 512-pixel step: 72 barriers per 128x128 unit).
+// Without `prob`, a pixel whose logit is below the threshold's (with a
+// margin) is staged as -1 without its sigmoid: such a pixel can neither be a
+// candidate nor beat one (its p < thr <= the candidate's p); NaN stays NaN.
 constexpr int PNT = 512;                // threads per unit block
 constexpr int PNW = PNT / 64;           // waves
-constexpr int PCHUNK = 2048;            // staged pixels per chunk (whole rows)
+constexpr int PCHUNK = 4096;            // staged pixels per chunk (whole rows)
+constexpr int PSTEPS = 32;              // 512-pixel steps per chunk at most (W <= 16384)
 
 __host__ __device__ inline int peak_rows(int W) { return W >= PCHUNK ? 1 : PCHUNK / W; }
 
@@ -91,36 +94,43 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o,
                                                     float *__restrict__ box, float *__restrict__ ref,
                                                     int32_t *__restrict__ counts, ExpTable et) {
     extern __shared__ float sp[];  // [R + 2][W] probabilities, row 0 = image row r0 - 1
-    __shared__ int wcnt[PNW];
+    __shared__ uint64_t bal[PSTEPS][PNW];
     const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const tmr_peak_param_t pp = params[u];
     const int HW = H * W, R = peak_rows(W);
     const float *ou = o + (size_t)u * HW;
-    float *pu = prob + (size_t)u * HW;
-    const float *r = reg ? reg + (size_t)u * 4 * HW : nullptr;
+    float *pu = prob ? prob + (size_t)u * HW : nullptr;
     const size_t cap = (size_t)HW;
-    const float sx = pp.mode == 1 ? 1.0f : pp.scale_w, sy = pp.mode == 1 ? 1.0f : pp.scale_h;
+    // logits below olo have sigmoid < thr by a wide margin (prob not asked)
+    float olo = -INFINITY;
+    if (!is_prob && !pu && pp.thr > 0.0f) {
+        const double t = (double)pp.thr;
+        const double lg = t < 1.0 ? log(t / (1.0 - t)) : 15.0;
+        olo = (float)(lg - 1e-3 * (1.0 + fabs(lg)));
+    }
+    const uint64_t lt = (1ull << lane) - 1ull;  // lanes below this one
     int base = 0;  // candidates so far (block-uniform)
     for (int r0 = 0; r0 < H; r0 += R) {
-        const int rn = min(R, H - r0), np = rn * W;
+        const int rn = min(R, H - r0), np = rn * W, ns = (np + PNT - 1) / PNT;
+#pragma unroll 4
         for (int e = tid; e < (rn + 2) * W; e += PNT) {
             const int lr = e / W, c = e - lr * W, y = r0 - 1 + lr;
             float v = 0.0f;
             if (y >= 0 && y < H) {
                 const float x = ou[(size_t)y * W + c];
-                v = is_prob ? x : tmr_sigmoid_cr(x);
-                if (lr >= 1 && lr <= rn) pu[(size_t)y * W + c] = v;
+                v = is_prob ? x : (x < olo ? -1.0f : tmr_sigmoid_cr(x));
+                if (pu && lr >= 1 && lr <= rn) pu[(size_t)y * W + c] = v;
             }
             sp[e] = v;
         }
-        __syncthreads();
-        for (int s0 = 0; s0 < np; s0 += PNT) {
-            const int i = s0 + tid;  // pixel of the chunk
-            const int ly = i / W + 1, x = i - (ly - 1) * W;
+        __syncthreads();  // (1) the chunk is staged
+        uint32_t fb = 0;  // bit s: this lane's pixel of step s is a candidate
+        for (int st = 0; st < ns; ++st) {
+            const int i = st * PNT + tid;  // pixel of the chunk
             bool f = false;
-            float v = 0.0f;
             if (i < np) {
-                v = sp[ly * W + x];
+                const int ly = i / W + 1, x = i - (ly - 1) * W;
+                const float v = sp[ly * W + x];
                 if (v >= pp.thr) {  // masked 3x3 max (TM_utils.py:337-361): first tap, then strict >
                     float mx = 0.0f;
                     bool first = true;
@@ -136,29 +146,32 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o,
                     f = mx == v;
                 }
             }
-            const uint64_t bal = __ballot(f);
-            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            if (lane == 0) wcnt[wave] = __popcll(bal);
-            __syncthreads();
-            int wbase = 0, tot = 0;
+            const uint64_t bw = __ballot(f);
+            if (lane == 0) bal[st][wave] = bw;
+            fb |= (uint32_t)f << st;
+        }
+        __syncthreads();  // (2) every step's ballots are in
+        int before = 0, tot = 0;  // candidates of the chunk before this wave's step st
+        for (int st = 0; st < ns; ++st) {
+            int cw = 0;
 #pragma unroll
             for (int k = 0; k < PNW; ++k) {
-                const int c = wcnt[k];
-                wbase += k < wave ? c : 0;
+                const int c = __popcll(bal[st][k]);
+                cw += k < wave ? c : 0;
                 tot += c;
             }
-            if (f) {  // the slot's pixel index rides in the box row until decode_kernel
-                const int y = r0 + ly - 1;
-                const size_t k = (size_t)u * cap + base + wbase + slot;
-                *reinterpret_cast<float2 *>(logits + 2 * k) = float2{v, 0.0f};
+            if ((fb >> st) & 1u) {  // the slot's pixel index rides in the box row until decode_kernel
+                const int i = st * PNT + tid, ly = i / W + 1, x = i - (ly - 1) * W, y = r0 + ly - 1;
+                const size_t k = (size_t)u * cap + base + before + cw + __popcll(bal[st][wave] & lt);
+                *reinterpret_cast<float2 *>(logits + 2 * k) = float2{sp[ly * W + x], 0.0f};
                 reinterpret_cast<int *>(box)[4 * k] = y * W + x;
                 *reinterpret_cast<float2 *>(ref + 2 * k) = float2{(float)x / (float)W, (float)y / (float)H};
             }
-            base += tot;
-            __syncthreads();  // wcnt (and, after the last step, sp) free again
+            before = tot;
         }
+        base += tot;
+        __syncthreads();  // (3) sp and the ballots free again
     }
-    (void)r; (void)sx; (void)sy;
     if (tid == 0) {
         counts[u] = base;
         if (base == 0) {  // the empty unit's dummy row (TM_utils.py:288-291) at row 0
@@ -167,6 +180,7 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ o,
             *reinterpret_cast<float2 *>(ref + (size_t)u * cap * 2) = float2{0.0f, 0.0f};
         }
     }
+    (void)reg; (void)et;
 }
 
 // The box decode of every candidate (TM_utils.py:264-278), chip-wide: one
@@ -216,7 +230,7 @@ extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *
                                 int W, const tmr_peak_param_t *params, float *prob, float *logits,
                                 float *box, float *ref, int32_t *counts, const void *exp_table,
                                 void *stream) {
-    TMR_REQUIRE(o && params && prob && logits && box && ref && counts && U > 0 && H > 0 && W > 0);
+    TMR_REQUIRE(o && params && logits && box && ref && counts && U > 0 && H > 0 && W > 0);
     hipStream_t s = tmr_stream(stream);
     ExpTable et = {nullptr, nullptr};
     if (exp_table) {

@@ -1271,9 +1271,10 @@ class TMREngine:
 
     @staticmethod
     def peaks(o: torch.Tensor, b: Optional[torch.Tensor], params: np.ndarray,
-              input_is_prob: bool = False):
-        """Peak finder + decode per unit -> (logits, box, ref, counts) with
-        per-unit stride H*W."""
+              input_is_prob: bool = False, want_prob: bool = True):
+        """Peak finder + decode per unit -> (logits, box, ref, counts, prob)
+        with per-unit stride H*W; prob is None unless want_prob (without it
+        the kernel skips the sigmoid of pixels that cannot matter)."""
         require_gpu(o, "objectness")
         o = o.float().contiguous()
         U = o.shape[0]
@@ -1281,7 +1282,7 @@ class TMREngine:
         dev = o.device
         cap = H * W
         prm = _h2d(params.view(np.uint8), dev, tag="peak_params")
-        prob = torch.empty((U, H, W), device=dev, dtype=torch.float32)
+        prob = torch.empty((U, H, W), device=dev, dtype=torch.float32) if want_prob else None
         logits = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         box = torch.empty((U * cap, 4), device=dev, dtype=torch.float32)
         ref = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
@@ -1289,7 +1290,8 @@ class TMREngine:
         bb = b.float().contiguous() if b is not None else None
         tab = exp_table.device_table(dev) if TMREngine.exp_mode == "reference" else None
         call("tmr_peaks_decode", ptr(o), int(input_is_prob), ptr(bb) if bb is not None else None,
-             U, H, W, ptr(prm), ptr(prob), ptr(logits), ptr(box), ptr(ref), ptr(counts),
+             U, H, W, ptr(prm), ptr(prob) if prob is not None else None, ptr(logits), ptr(box), ptr(ref),
+             ptr(counts),
              ptr(tab) if tab is not None else None, stream())
         return logits, box, ref, counts, prob
 
@@ -1390,7 +1392,7 @@ class TMREngine:
         also the device-sized small NMS (tmr_nms_small) and one int32 tensor
         [counts..., kept...] to read back with a single sync."""
         r = self.forward_units(feats, unit_image, boxes)
-        logits, box, ref, counts, _ = self.peaks(r["o"], r["b"], params)
+        logits, box, ref, counts, _ = self.peaks(r["o"], r["b"], params, want_prob=False)
         if nms is None:
             return logits, box, ref, counts
         unit_off, seg, iou = nms

@@ -101,7 +101,7 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         H, W = o.shape[-2:]
         reg = pred_regressions[level] if (box_reg and pred_regressions is not None) else None
         params = host.peak_params(boxes, H, W, cls_ths, box_reg, ab_b, ab_c)
-        logits, box, ref, counts, _ = TMREngine.peaks(o, reg, params, input_is_prob)
+        logits, box, ref, counts, _ = TMREngine.peaks(o, reg, params, input_is_prob, want_prob=False)
         counts = counts.cpu().numpy()  # torch.where's sync (TM_utils.py:254)
         cap = H * W
         per_level.append([(logits[b * cap:b * cap + counts[b]], box[b * cap:b * cap + counts[b]],

@@ -1134,6 +1134,45 @@ def test_xcorr_mfma_lds_fragments_bitexact(prec, H, W, kmax):
         assert bits_equal(res["lds"][t], res["split"][t]), (prec, t)
 
 
+@pytest.mark.parametrize("thr", [0.1, 0.5, 0.999, 1.0, 0.0])
+def test_peaks_without_prob_match_with_prob(thr):
+    """TMREngine.peaks without the probability map (detect, Get_pred_boxes)
+    stages a logit well below the threshold's as -1 instead of its sigmoid:
+    the candidates, their order, logits, refs and boxes are bit-identical to
+    the run that writes prob -- logits straddling logit(thr) by ulps, NaN
+    and +-inf logits, saturated maps, every mask shape, W of 64 / 96 / 130
+    (whole-row chunks of different heights)."""
+    for H, W in ((64, 64), (48, 96), (33, 130)):
+        U = 6
+        o = (synth.normal(811 + W, (U, 1, H, W)) * 3.0).astype(np.float32)
+        if 0.0 < thr < 1.0:
+            lg = np.float32(np.log(thr / (1.0 - thr)))
+            away = np.where(np.arange(40) % 2, 1e9, -1e9).astype(np.float32)
+            near = np.nextafter(np.full(40, lg, np.float32), away)
+            o[0, 0, 5, :40] = near
+            o[1, 0, 7, 3:43] = lg
+        o[2, 0, 3, 4] = np.nan
+        o[2, 0, 9, 9] = np.inf
+        o[2, 0, 11, 2] = -np.inf
+        o[3] = 40.0  # saturated: p == 1 everywhere (ties)
+        reg = (synth.normal(812 + W, (U, 4, H, W)) * 0.3).astype(np.float32)
+        side = np.array([1.5, 4.0, 9.0, 1.5, 4.0, 9.0], np.float32)
+        boxes = np.stack([np.full(U, 0.2, np.float32), np.full(U, 0.3, np.float32),
+                          0.2 + side / W, 0.3 + side / H], 1).astype(np.float32)
+        params = host.peak_params(boxes, H, W, thr)
+        a = tmr_amd.TMREngine.peaks(cuda(o), cuda(reg), params, want_prob=True)
+        b = tmr_amd.TMREngine.peaks(cuda(o), cuda(reg), params, want_prob=False)
+        assert b[4] is None
+        ca, cb = a[3].cpu().numpy(), b[3].cpu().numpy()
+        assert np.array_equal(ca, cb), (H, W, thr)
+        for t in range(3):
+            x, y = a[t].cpu().numpy(), b[t].cpu().numpy()
+            rows = x.reshape(U, H * W, -1), y.reshape(U, H * W, -1)
+            for u in range(U):
+                k = max(int(ca[u]), 1)
+                assert bits_equal(rows[0][u, :k], rows[1][u, :k]), (H, W, thr, t, u)
+
+
 def test_nms_worst_case_dense_candidates():
     """SURVEY.md §7.3.3 worst case: a centre-only adaptive kernel (exemplars
     under 2 px) with p ~ 0.5 everywhere at cls 0.1 makes EVERY pixel a
