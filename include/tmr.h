@@ -319,13 +319,16 @@ int tmr_maxpool3x3(const float *x, int64_t planes, int H, int W, int mask9, floa
  * box[(u*cap+i)*4] (normalised xyxy), ref[(u*cap+i)*2], counts[u]; a unit
  * with no peak (counts[u] = 0) gets the reference's dummy row at its row 0
  * (logits (0,0), box (0,0,1e-14,1e-14), ref (0,0); TM_utils.py:288-291).
- * prob [U,H,W] receives the probability map, or NULL: not written (and the
- * sigmoid of pixels whose logit lies well below the threshold is skipped).
+ * prob [U,H,W] receives the probability map (required).  With
+ * TMR_PEAKS_PROB_SCRATCH or-ed into input_is_prob it is scratch only: a
+ * pixel whose logit lies well below its unit's threshold holds -1 there (its
+ * sigmoid is skipped); the candidates are the same.
  * exp_table (device, nullable): the reference-exp table (tmr_amd/exp_table.py:
  * 128-B header, uint32 offsets[65537], sorted uint16 low halves).  The decode's
  * exp (TM_utils.py:272) is the correctly rounded value except at the table's
  * inputs, where it is the other neighbour, as the reference's torch.exp (MKL
  * vsExp) rounds; NULL = correctly rounded everywhere. */
+#define TMR_PEAKS_PROB_SCRATCH 2  /* input_is_prob flag: prob is scratch (see above) */
 int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U, int H, int W,
                      const tmr_peak_param_t *params, float *prob, float *logits, float *box,
                      float *ref, int32_t *counts, const void *exp_table, void *stream);

@@ -46,6 +46,7 @@ SPLIT_TILED_OUT, SPLIT_TILED_INIT, SPLIT_INIT_BCAST = 1, 2, 4
 SPLIT_OUT_BF16, SPLIT_INIT_BF16 = 8, 16  # one-term precisions: bf16 acc0 slabs
 SPLIT_XMAX_PER_UNIT = 32  # xmax is float[U]: one activation scale per unit / output slab
 SPLIT_XMAX_PER_PIXEL = 64  # 1x1 stores: xmax is float[U][H][W], one scale per output pixel
+PEAKS_PROB_SCRATCH = 2  # tmr_peaks_decode: prob is scratch (low logits hold -1)
 SPLIT_UNITS_PER_IMAGE_SHIFT = 8  # flags bits 8..15: E units per image -> image-major heads order
 # correlation kernel choice (tmr_xcorr_algo)
 XCORR_ALGOS = {"auto": 0, "valu": 1, "mfma": 2}

@@ -31,8 +31,9 @@ import numpy as np
 import torch
 
 from . import exp_table, host
-from ._lib import (PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
-                   SPLIT_TILED_OUT, SPLIT_UNITS_PER_IMAGE_SHIFT, SPLIT_XMAX_PER_PIXEL, SPLIT_XMAX_PER_UNIT,
+from ._lib import (PEAKS_PROB_SCRATCH, PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16,
+                   SPLIT_TILED_INIT, SPLIT_TILED_OUT, SPLIT_UNITS_PER_IMAGE_SHIFT, SPLIT_XMAX_PER_PIXEL,
+                   SPLIT_XMAX_PER_UNIT,
                    UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr,
                    require_gpu, stream)
 
@@ -786,6 +787,10 @@ class TMREngine:
         # by the correlation, so a quiet region of an image must keep its
         # own fp32-grade precision (tests/test_gpu_precision.py (b))
         xmax = None if pprec == "bf16" else pixel_absmax(feats)
+        if xmax is not None and self.cfg.precision != "bf16":
+            # max |f| per image (the fp half's record scale, _feat_absmax) is
+            # the max of these per-pixel maxima: no second read of the features
+            self._memo_absmax(feats, "feat", lambda: absmax_rows(xmax))
         # the 1x1 projection commutes with the bilinear x2 (both linear;
         # the interpolation weights of each output sum to 1, so the bias
         # passes through): project at the features' size, then upsample
@@ -1282,18 +1287,18 @@ class TMREngine:
         dev = o.device
         cap = H * W
         prm = _h2d(params.view(np.uint8), dev, tag="peak_params")
-        prob = torch.empty((U, H, W), device=dev, dtype=torch.float32) if want_prob else None
+        prob = torch.empty((U, H, W), device=dev, dtype=torch.float32)  # (scratch unless want_prob)
         logits = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         box = torch.empty((U * cap, 4), device=dev, dtype=torch.float32)
         ref = torch.empty((U * cap, 2), device=dev, dtype=torch.float32)
         counts = torch.empty(U, device=dev, dtype=torch.int32)
         bb = b.float().contiguous() if b is not None else None
         tab = exp_table.device_table(dev) if TMREngine.exp_mode == "reference" else None
-        call("tmr_peaks_decode", ptr(o), int(input_is_prob), ptr(bb) if bb is not None else None,
-             U, H, W, ptr(prm), ptr(prob) if prob is not None else None, ptr(logits), ptr(box), ptr(ref),
-             ptr(counts),
+        flags = int(input_is_prob) | (0 if want_prob else PEAKS_PROB_SCRATCH)
+        call("tmr_peaks_decode", ptr(o), flags, ptr(bb) if bb is not None else None,
+             U, H, W, ptr(prm), ptr(prob), ptr(logits), ptr(box), ptr(ref), ptr(counts),
              ptr(tab) if tab is not None else None, stream())
-        return logits, box, ref, counts, prob
+        return logits, box, ref, counts, (prob if want_prob else None)
 
     @staticmethod
     def nms(logits, box, ref, counts: torch.Tensor, counts_host: np.ndarray,
