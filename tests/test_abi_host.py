@@ -94,6 +94,11 @@ def test_invalid_arguments_return_codes():
     assert L.tmr_maxpool3x3(None, 1, 4, 4, 0, None, None) == -1
     assert L.tmr_maxpool3x3(None, 1, 4, 4, 1 << 9, None, None) == -1
     assert L.tmr_maxpool3x3(None, 0, 4, 4, 0x1ff, None, None) == 0  # empty input: nothing to launch
+    # peaks: prob is required (scratch with TMR_PEAKS_PROB_SCRATCH); unknown flag bits are refused
+    buf = np.zeros(16, np.float32)
+    a = buf.ctypes.data
+    assert L.tmr_peaks_decode(a, 0, None, 1, 2, 2, a, None, a, a, a, a, None, None) == -1
+    assert L.tmr_peaks_decode(a, 4, None, 1, 2, 2, a, a, a, a, a, a, None, None) == -1
 
 
 def test_tm_utils_host_helpers():
