@@ -563,6 +563,13 @@ class _DetectGraph:
         return self.outputs
 
 
+# the heads launch's image-major block order (an image's units innermost) for
+# up to this many units per image: config B (3 per image) 106.6 -> 106.0 ms
+# (profiles/r05c), config E (16 per image) 166.6 -> 168.5 ms (profiles/r05t).
+# A/B knob TMR_HEADS_IMAGE_MAJOR_MAX (the flags field holds <= 255)
+HEADS_IMAGE_MAJOR_MAX = min(255, int(os.environ.get("TMR_HEADS_IMAGE_MAJOR_MAX", "4")))
+
+
 class TMREngine:
     """Native forward + post-processing over (image, exemplar) units."""
 
@@ -1113,7 +1120,7 @@ class TMREngine:
         then runs image-major, TMR_SPLIT_UNITS_PER_IMAGE_SHIFT), else 1."""
         U = len(unit_image)
         E = U // max(B, 1)
-        if E <= 1 or E > 255 or E * B != U:
+        if E <= 1 or E > HEADS_IMAGE_MAJOR_MAX or E * B != U:
             return 1
         ui = np.asarray(unit_image)
         return E if np.array_equal(ui, np.repeat(np.arange(B), E)) else 1
