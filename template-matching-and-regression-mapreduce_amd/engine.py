@@ -1367,7 +1367,7 @@ class TMREngine:
     # the same launch signature recurs (the reference's per-image loop at one
     # image size and recurring template sizes): the host then issues ONE
     # launch instead of ~30, and the GPU no longer idles while Python prepares
-    # them (config A: 0.38 of 2.95 ms per image, profiles/r04b/).  A signature
+    # them (config A: 0.38 of 2.95 ms per image, profiles/archive/r04b/).  A signature
     # is captured the second time it is seen; up to GRAPH_MAX_UNITS units (the
     # graph's memory pool holds every intermediate) and GRAPH_CACHE entries.
     use_graphs = True

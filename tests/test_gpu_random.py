@@ -15,7 +15,7 @@ the oracle exactly as the headline tests check the graded batches:
 
 The configurations are drawn from a fixed seed, so the sweep is the same on
 every run; the default 200 + 200 take a few seconds.  TMR_RANDOM_SWEEP=N
-widens both sweeps to N seeds (a one-off deep run, e.g. profiles/r04_random*.log).
+widens both sweeps to N seeds (a one-off deep run, e.g. profiles/archive/r04_random*.log).
 """
 import os
 
