@@ -18,6 +18,7 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   imgmajor an image's 3 units innermost in the heads grid (acc0 tile reuse; a correct build
            for 3 units per image)
+  uprN     the upsample's output tile at N rows (32 committed; correct builds)
   gnolist / gnochain / gnorescan   the NMS greedy wave without its list test / its
            in-block chain / its overflow rescan (wrong keep lists; greedy_kernel time only)
   l2dma    every DMA re-reads the first chunk's halo / first step's weights:
@@ -113,6 +114,8 @@ def variant_source(name: str, src: str) -> str:
             u = L / per_unit;
             r = L - u * per_unit;
         }""")
+    if name.startswith("upr"):  # upsample2x output tile rows (upr64, upr128)
+        return _sub(src, "constexpr int UPT_R = 32, UPT_C = 128;", f"constexpr int UPT_R = {int(name[3:])}, UPT_C = 128;")
     if name == "gnolist":
         return _sub(src, "        bool rem = rem32 != 0;", "        bool rem = false; (void)rem32;")
     if name == "gnochain":
@@ -127,6 +130,8 @@ def variant_source(name: str, src: str) -> str:
 def variant_file(name: str) -> str:
     if name.startswith("g"):
         return "nms.hip"
+    if name.startswith("upr"):
+        return "upsample_heads.hip"
     return "xcorr.hip" if name.startswith(("tsparse", "xl2band", "xl2a")) else "conv_split.hip"
 
 
