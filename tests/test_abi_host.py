@@ -99,6 +99,10 @@ def test_invalid_arguments_return_codes():
     a = buf.ctypes.data
     assert L.tmr_peaks_decode(a, 0, None, 1, 2, 2, a, None, a, a, a, a, None, None) == -1
     assert L.tmr_peaks_decode(a, 4, None, 1, 2, 2, a, a, a, a, a, a, None, None) == -1
+    # NMS: an image beyond the greedy wave's LDS bitmap (655,360 candidates) is refused, not truncated
+    big = 700_000
+    assert L.tmr_nms(a, a, a, a, a, a, a, a, 1, big, big, (big + 63) // 64, 0.5, a, a, a, None, a, a,
+                     None) == -1
 
 
 def test_tm_utils_host_helpers():
