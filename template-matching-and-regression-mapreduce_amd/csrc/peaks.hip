@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256) void prob_kernel(const float *__restrict__ o, 
 // step: 72 barriers per 128x128 unit).
 constexpr int PNT = 1024;               // threads per unit block (16 waves: one unit per CU at most)
 constexpr int PNW = PNT / 64;           // waves
-constexpr int PCHUNK = 4096;            // staged pixels per chunk (whole rows)
-constexpr int PSTEPS = 16;              // PNT-pixel steps per chunk at most (W <= 16384)
+constexpr int PCHUNK = 16384;           // staged pixels per chunk (whole rows): a 128 x 128 map in one
+constexpr int PSTEPS = PCHUNK / PNT;    // PNT-pixel steps per chunk at most (W <= PCHUNK / 2)
 
 __host__ __device__ inline int peak_rows(int W) { return W >= PCHUNK ? 1 : PCHUNK / W; }
 
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ pm
     const int u = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const tmr_peak_param_t pp = params[u];
     const int HW = H * W, R = peak_rows(W);
-    // e / W by one multiply: exact while e < (R + 2) W <= 3 * 16384 (rows < 2^22 / W)
+    // e / W by one multiply: exact while e < (R + 2) W <= 2 * PCHUNK (far below 2^22)
     const float rW = 1.0f / (float)W;
     const float *pmu = pm + (size_t)u * HW;
     const size_t cap = (size_t)HW;
@@ -277,7 +277,7 @@ extern "C" int tmr_peaks_decode(const float *o, int input_is_prob, const float *
         et.off = reinterpret_cast<const uint32_t *>(base + EXP_HEADER);
         et.lo = reinterpret_cast<const uint16_t *>(base + EXP_HEADER + 4 * 65537);
     }
-    TMR_REQUIRE(W <= 16384);
+    TMR_REQUIRE(W <= PCHUNK / 2);  // (R + 2) W floats of LDS <= 3 * 8192 * 4 B
     const size_t lds = (size_t)(peak_rows(W) + 2) * W * sizeof(float);
     if (lds > 64 * 1024 && tmr_set_max_lds((const void *)peaks_kernel, lds) != hipSuccess) return TMR_E_HIP;
     const float *pm = o;
