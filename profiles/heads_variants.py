@@ -18,6 +18,8 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   imgmajor an image's 3 units innermost in the heads grid (acc0 tile reuse; a correct build
            for 3 units per image)
+  xring0   the correlation's A fragments copied out of their prefetch slots (round-4 loop)
+  xpf3_N / xpfwN   the correlation's A-fragment ring at N slots (3-term; < 6 / >= 6 tiles per wave)
   uprN     the upsample's output tile at N rows (32 committed; correct builds)
   gnolist / gnochain / gnorescan   the NMS greedy wave without its list test / its
            in-block chain / its overflow rescan (wrong keep lists; greedy_kernel time only)
@@ -114,6 +116,12 @@ def variant_source(name: str, src: str) -> str:
             u = L / per_unit;
             r = L - u * per_unit;
         }""")
+    if name == "xring0":  # the correlation's A fragments copied out of the prefetch slots (round 4 form)
+        return _sub(src, "constexpr int XCORR_RING = 1;", "constexpr int XCORR_RING = 0;")
+    if name.startswith("xpf3_"):  # ring slots of the 3-term kernel below 6 tiles per wave
+        return _sub(src, "constexpr int XRING_PF1 = 4, XRING_PF3 = 2,", f"constexpr int XRING_PF1 = 4, XRING_PF3 = {int(name[5:])},")
+    if name.startswith("xpfw"):  # ring slots of the 3-term kernel at >= 6 tiles per wave
+        return _sub(src, "XRING_PF3_WIDE = 3;", f"XRING_PF3_WIDE = {int(name[4:])};")
     if name.startswith("upr"):  # upsample2x output tile rows (upr64, upr128)
         return _sub(src, "constexpr int UPT_R = 32, UPT_C = 128;", f"constexpr int UPT_R = {int(name[3:])}, UPT_C = 128;")
     if name == "gnolist":
@@ -132,7 +140,7 @@ def variant_file(name: str) -> str:
         return "nms.hip"
     if name.startswith("upr"):
         return "upsample_heads.hip"
-    return "xcorr.hip" if name.startswith(("tsparse", "xl2band", "xl2a")) else "conv_split.hip"
+    return "xcorr.hip" if name.startswith(("tsparse", "xl2band", "xl2a", "xring", "xpf")) else "conv_split.hip"
 
 
 VARIANTS = ["nobar", "nowait", "noacc0", "noepi", "nodma", "l2dma"]
