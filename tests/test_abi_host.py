@@ -428,3 +428,17 @@ def test_graph_book_bounded_and_failures_remembered():
     b.clear()
     assert not (b.graphs or b.seen or b.failed)
     assert TMREngine.GRAPH_CACHE >= 1
+
+
+def test_heads_image_major_only_for_few_units_per_image():
+    """The heads launch runs image-major (an image's units innermost) up to
+    HEADS_IMAGE_MAJOR_MAX units per image (config B's 3: faster; config E's
+    16: 1.1% slower, profiles/r05t), and only for units in image order."""
+    from tmr_amd import engine
+    upi = engine.TMREngine._units_per_image
+    assert engine.HEADS_IMAGE_MAJOR_MAX == 4
+    assert upi(np.repeat(np.arange(64), 3), 64) == 3
+    assert upi(np.repeat(np.arange(8), 16), 8) == 1
+    assert upi(np.arange(64), 64) == 1                    # one unit per image
+    assert upi(np.array([0, 1, 0, 1, 0, 1]), 2) == 1      # not in image order
+
