@@ -1,0 +1,15 @@
+# Round 5, call z2: config B, heads XCD block groups 8 x 4 (committed) vs
+# 2 x 16 and 1 x 32, three reps alternating.
+# Run from the repo root: gpurun -- bash profiles/gpu_r05z2.sh
+set -o pipefail
+O=gpurun_out/r05z2
+mkdir -p $O
+export TMPDIR=/tmp
+b() {  # b <tag> <variant> <config>
+  if [ $2 = base ]; then unset TMR_LIB_VARIANT; else export TMR_LIB_VARIANT=$2; fi
+  timeout -k 10 200 python bench.py --config $3 --no-cpu-baseline --no-xcorr-classes > $O/$1.json 2> $O/$1.err || { echo "BENCH_FAILED $1"; tail -5 $O/$1.err; return 1; }
+  python -c "import json;d=json.load(open('$O/$1.json'));print('$1',d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'])"
+}
+for rep in 1 2 3; do for v in base pxg2 pxg1; do b B_${v}_$rep $v B || exit 1; done; done
+for v in base pxg2; do b C_$v $v C && b D_$v $v D || exit 1; done
+echo done

@@ -18,6 +18,7 @@ heads launch time (roofline.avg_launch_ms) and the PMC counters mean anything.
            N significant bits (WH_BITS / TH_BITS; these ARE correct builds)
   imgmajor an image's 3 units innermost in the heads grid (acc0 tile reuse; a correct build
            for 3 units per image)
+  pxgN     the heads launch's XCD block groups at N pixel tiles x 32/N channel tiles (8 x 4 committed)
   xring0   the correlation's A fragments copied out of their prefetch slots (round-4 loop)
   xpf3_N / xpfwN   the correlation's A-fragment ring at N slots (3-term; < 6 / >= 6 tiles per wave)
   uprN     the upsample's output tile at N rows (32 committed; correct builds)
@@ -116,6 +117,9 @@ def variant_source(name: str, src: str) -> str:
             u = L / per_unit;
             r = L - u * per_unit;
         }""")
+    if name.startswith("pxg"):  # heads XCD block groups: PXG pixel tiles x (32 / PXG) channel tiles
+        pxg = int(name[3:])
+        return _sub(src, "constexpr int PXG = 8, NG = 4;", f"constexpr int PXG = {pxg}, NG = {32 // pxg};")
     if name == "xring0":  # the correlation's A fragments copied out of the prefetch slots (round 4 form)
         return _sub(src, "constexpr int XCORR_RING = 1;", "constexpr int XCORR_RING = 0;")
     if name.startswith("xpf3_"):  # ring slots of the 3-term kernel below 6 tiles per wave
