@@ -629,6 +629,7 @@ class TMREngine:
         self._fp_memo = None
         self._acc0_memo = None
         self._graphs = _GraphBook(self.GRAPH_CACHE)
+        self._pnames = None
         self.last_graph = None
         self.last_graph_error = None
         self.last_decoder_flops = 0.0
@@ -1386,7 +1387,20 @@ class TMREngine:
                 self.fold_proj,
                 self.share_fp_half, self.xcorr_algo, self.out_bf16, TMREngine.exp_mode,
                 bool(ablation_b), bool(ablation_c),
-                tuple((k, t.data_ptr(), t._version) for k, t in sorted(self.P.items())))
+                self._param_key())
+
+    def _param_key(self):
+        """(name, storage, version) of every parameter, in name order (the
+        sorted names cached while the dict keeps its key set)."""
+        P = self.P
+        names = self._pnames
+        if names is None or names[1] is not P or len(names[0]) != len(P):
+            names = self._pnames = (tuple(sorted(P)), P)
+        try:
+            return tuple((k, P[k].data_ptr(), P[k]._version) for k in names[0])
+        except KeyError:  # a key replaced by another: re-sort
+            self._pnames = None
+            return self._param_key()
 
     @staticmethod
     def _detect_host_inputs(units, unit_image, B, params, nms_in=None) -> Dict[str, np.ndarray]:

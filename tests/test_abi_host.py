@@ -6,6 +6,7 @@ import re
 
 import numpy as np
 import pytest
+import torch
 
 import oracle
 import tmr_amd
@@ -441,4 +442,23 @@ def test_heads_image_major_only_for_few_units_per_image():
     assert upi(np.repeat(np.arange(8), 16), 8) == 1
     assert upi(np.arange(64), 64) == 1                    # one unit per image
     assert upi(np.array([0, 1, 0, 1, 0, 1]), 2) == 1      # not in image order
+
+
+def test_graph_param_key_follows_the_parameter_dict():
+    """The graph signature's parameter part (TMREngine._param_key): name
+    order cached, but versions, replaced tensors, added and swapped keys all
+    show in the key (a stale key would replay a graph on old weights)."""
+    P = {"b": torch.zeros(2), "a": torch.ones(3)}
+    e = tmr_amd.TMREngine(P, tmr_amd.PathConfig())
+    k1 = e._param_key()
+    assert [x[0] for x in k1] == ["a", "b"]
+    P["a"].add_(1)
+    assert e._param_key() != k1                       # in-place update: new version
+    P["a"] = torch.ones(3)
+    assert e._param_key()[0][1] == P["a"].data_ptr()  # replaced tensor
+    del P["b"]
+    P["c"] = torch.zeros(1)
+    assert [x[0] for x in e._param_key()] == ["a", "c"]  # same count, other key
+    P["d"] = torch.zeros(1)
+    assert [x[0] for x in e._param_key()] == ["a", "c", "d"]
 
