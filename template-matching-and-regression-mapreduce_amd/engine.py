@@ -20,6 +20,7 @@ MFMA layouts are derived caches, rebuilt when a parameter changes.
 """
 from __future__ import annotations
 
+import gc
 import json
 import os
 import threading
@@ -568,6 +569,25 @@ class _DetectGraph:
 # (profiles/r05c), config E (16 per image) 166.6 -> 168.5 ms (profiles/r05t).
 # A/B knob TMR_HEADS_IMAGE_MAJOR_MAX (the flags field holds <= 255)
 HEADS_IMAGE_MAJOR_MAX = min(255, int(os.environ.get("TMR_HEADS_IMAGE_MAJOR_MAX", "4")))
+
+
+class _no_gc:
+    """Python's cyclic GC off for the length of a graph capture: a collection
+    inside the capture can destroy an unreachable object that owns a HIP
+    event or graph (an evicted replay's), and a destroy call during a global
+    capture aborts the process (seen once in test_module_graph_replays_back_to_back,
+    profiles/r05aa).  torch.cuda.graph collects on entry; this keeps it off
+    until the capture has ended."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
 
 
 class TMREngine:
@@ -1211,7 +1231,7 @@ class TMREngine:
         graph = torch.cuda.CUDAGraph()
         _capture.blob = blob
         try:
-            with torch.cuda.graph(graph):
+            with _no_gc(), torch.cuda.graph(graph):
                 blob.upload()
                 out = self._forward_units_eager(static, unit_image, boxes, want_aux)
             fp_acc0 = (self._fp_memo[4], self._acc0_memo[3:6]) if hit is None else (None, None)
@@ -1443,7 +1463,7 @@ class TMREngine:
         graph = torch.cuda.CUDAGraph()
         _capture.blob = blob
         try:
-            with torch.cuda.graph(graph):
+            with _no_gc(), torch.cuda.graph(graph):
                 blob.upload()
                 out = self._forward_peaks(static, unit_image, boxes, params, nms)
         except Exception as err:  # noqa: BLE001 -- a launch this HIP runtime cannot capture: stay eager
