@@ -107,8 +107,7 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         per_level.append([(logits[b * cap:b * cap + counts[b]], box[b * cap:b * cap + counts[b]],
                            ref[b * cap:b * cap + counts[b]]) for b in range(B)])
         if level == 0:  # an empty unit's row 0 holds the dummy row (tmr_peaks_decode)
-            dummies = [(logits[b * cap:b * cap + 1], box[b * cap:b * cap + 1], ref[b * cap:b * cap + 1])
-                       for b in range(B)]
+            lv0 = (logits, box, ref, cap)
     pred_logits, pred_boxes, ref_points = [], [], []
     for b in range(B):
         parts = [lv[b] for lv in per_level]
@@ -120,8 +119,8 @@ def Get_pred_boxes(pred_objectness, pred_regressions, exemplars, batch, cls_ths=
         if lg.shape[0] == 0:  # every level empty: the dummy row, fresh 1-row tensors as the
             # reference's (TM_utils.py:288-291): cloned on the device (no sync), so a kept
             # dummy does not hold the call's [U*H*W] peak buffers alive
-            lg, bx, rf = (tuple(t.clone() for t in dummies[b]) if dtype == torch.float32
-                          else _dummy(dtype, device))
+            lg, bx, rf = (tuple(t[b * lv0[3]:b * lv0[3] + 1].clone() for t in lv0[:3])
+                          if dtype == torch.float32 else _dummy(dtype, device))
         pred_logits.append(lg); pred_boxes.append(bx); ref_points.append(rf)
     return pred_logits, pred_boxes, ref_points
 
