@@ -763,6 +763,56 @@ def test_nms_threshold_windows_vs_oracle(thr):
         assert bits_equal(L[k].cpu().numpy()[:, 0], sc[keep]), (thr, k)
 
 
+def _nms_sweep_image(r):
+    """One random image for the NMS sweep: a random count (small path and
+    binned path), box-size law (narrow, spread over decades, thin in one
+    axis, clustered near-duplicates), coordinate scale and offset, and score
+    quantisation (ties)."""
+    n = int(np.exp(r.uniform(np.log(2), np.log(20000))))
+    law = r.integers(0, 4)
+    xy = r.random((n, 2))
+    if law == 0:
+        wh = 0.003 + r.random((n, 2)) * 0.05
+    elif law == 1:
+        wh = 10.0 ** r.uniform(-3.5, -0.3, (n, 2))
+    elif law == 2:  # thin boxes: one side up to 200x the other
+        s = 10.0 ** r.uniform(-3, -1, (n, 1))
+        a = 10.0 ** r.uniform(-2.3, 0, (n, 1))
+        wh = np.where(r.random((n, 1)) < 0.5, np.concatenate([s, s * a], 1), np.concatenate([s * a, s], 1))
+    else:  # clusters of near-duplicates around a few centres
+        c = r.random((max(1, n // 50), 2))
+        xy = c[r.integers(0, len(c), n)] + r.normal(0, 0.004, (n, 2))
+        wh = 0.02 + r.random((n, 2)) * 0.01
+    scale = 10.0 ** r.uniform(-4, 4)
+    off = r.uniform(-1, 1) * scale * 10 ** r.integers(0, 3)
+    bx = (np.concatenate([xy, xy + wh], 1) * scale + off).astype(np.float32)
+    q = 2.0 ** r.integers(3, 24)
+    sc = (np.round(r.random(n) * q) / q).astype(np.float32)
+    return bx, sc
+
+
+def test_nms_random_sweep_vs_oracle():
+    """Seeded random calls (1-4 images each, TMR_NMS_SWEEP calls, default 60):
+    every image's keep list bit-exact vs the oracle's sequential torchvision
+    list, for a threshold drawn uniformly in (0, 1) per call (plus a few at
+    the narrowing cut-off 2^-12 and at 0.999)."""
+    import os
+    ncalls = int(os.environ.get("TMR_NMS_SWEEP", "60"))
+    r = np.random.default_rng(4242)
+    worst = 0
+    for call in range(ncalls):
+        thr = float(r.choice([2.0 ** -12, 0.999])) if call % 10 == 9 else float(r.uniform(0.001, 0.999))
+        imgs = [_nms_sweep_image(r) for _ in range(int(r.integers(1, 5)))]
+        L, Bx, R = tmr_amd.NMS([cuda(np.stack([sc, np.zeros_like(sc)], 1)) for bx, sc in imgs],
+                               [cuda(bx) for bx, sc in imgs], [cuda(bx[:, :2].copy()) for bx, sc in imgs], thr)
+        for k, (bx, sc) in enumerate(imgs):
+            keep = oracle.nms(bx, sc, thr)
+            assert bits_equal(Bx[k].cpu().numpy(), bx[keep]), (call, thr, k, len(bx), len(keep), Bx[k].shape[0])
+            assert bits_equal(L[k].cpu().numpy()[:, 0], sc[keep]), (call, thr, k)
+            worst = max(worst, len(bx))
+    print(f"nms sweep: {ncalls} calls, largest image {worst} candidates")
+
+
 def test_nms_binned_nonfinite_boxes_match_dense():
     """Non-finite box coordinates put the image in one bin (every pair
     evaluated with the kernels' own fmaxf/fminf arithmetic): an image of
