@@ -570,6 +570,71 @@ def test_get_pred_boxes_empty_units_dummy_row():
             assert np.array_equal(Bx[b].cpu().numpy(), np.array([[0, 0, 1e-14, 1e-14]], np.float32))
 
 
+def _peaks_sweep_case(r):
+    """One random Get_pred_boxes call: map shape (small, medium, one-row-wide
+    up to 8192 columns, tall and narrow, several LDS chunks), unit count,
+    logit law (near-ties around 0, plateaus, saturated, +-inf / NaN pixels),
+    exemplar boxes from sub-pixel to most of the map (every adaptive kernel
+    shape), threshold, box regression and the ablation flags."""
+    law = r.integers(0, 4)
+    if law == 0:
+        H, W = int(r.integers(1, 41)), int(r.integers(1, 41))
+    elif law == 1:
+        H, W = int(r.integers(41, 301)), int(r.integers(41, 301))
+    elif law == 2:
+        H, W = int(r.integers(1, 5)), int(r.integers(300, 8193))
+    else:
+        H, W = int(r.integers(300, 2001)), int(r.integers(1, 5))
+    U = int(r.integers(1, 7))
+    sig = float(r.choice([0.05, 1.0, 3.0, 10.0]))
+    o = (r.standard_normal((U, 1, H, W)) * sig).astype(np.float32)
+    if r.random() < 0.5:  # plateaus: exact ties between neighbours
+        q = float(r.choice([0.25, 1.0]))
+        o = (np.round(o / q) * q).astype(np.float32)
+    flat = o.reshape(-1)
+    k = max(1, flat.size // 500)
+    if r.random() < 0.3:
+        flat[r.integers(0, flat.size, k)] = 30.0
+    if r.random() < 0.3:
+        flat[r.integers(0, flat.size, k)] = np.float32(r.choice([np.inf, -np.inf, np.nan]))
+    reg = (r.standard_normal((U, 4, H, W)) * 0.5).astype(np.float32)
+    x1, y1 = r.uniform(-0.1, 0.9, U), r.uniform(-0.1, 0.9, U)
+    bw = 10.0 ** r.uniform(np.log10(0.25 / max(W, 1)), np.log10(0.8), U)
+    bh = 10.0 ** r.uniform(np.log10(0.25 / max(H, 1)), np.log10(0.8), U)
+    boxes = np.stack([x1, y1, x1 + bw, y1 + bh], 1).astype(np.float32)
+    thr = float(r.uniform(0.01, 0.99))
+    box_reg = bool(r.random() < 0.8)
+    ab = int(r.integers(0, 4))  # 0, 1: none; 2: ablation_b; 3: ablation_c
+    return o, reg, boxes, thr, box_reg, ab == 2, ab == 3
+
+
+def test_peaks_random_sweep_vs_oracle():
+    """Seeded random Get_pred_boxes calls (TMR_PEAKS_SWEEP, default 60): every
+    unit's candidate logits, boxes and reference points bit-exact vs the
+    oracle on the correctly rounded sigmoid of the same logits (the call
+    discards the probability map, so the kernel runs in its scratch mode)."""
+    import os
+    n = int(os.environ.get("TMR_PEAKS_SWEEP", "60"))
+    r = np.random.default_rng(5151)
+    npx = ncand = 0
+    for i in range(n):
+        o, reg, boxes, thr, box_reg, ab_b, ab_c = _peaks_sweep_case(r)
+        batch = {"regression_ablation_b": ab_b, "regression_ablation_c": ab_c}
+        L, Bx, R = tmr_amd.Get_pred_boxes([cuda(o)], [cuda(reg)] if box_reg else None,
+                                          [cuda(b[None]) for b in boxes], batch, thr, box_reg)
+        prob = oracle.sigmoid_cr(o)
+        oL, oB, oR = oracle.get_pred_boxes_prob(list(prob[:, 0]), list(reg) if box_reg else None,
+                                                [b[None] for b in boxes], thr, box_reg, ab_b, ab_c)
+        for b in range(len(boxes)):
+            meta = (i, b, o.shape, thr, box_reg, ab_b, ab_c)
+            assert bits_equal(L[b].cpu().numpy(), oL[b]), meta
+            assert bits_equal(Bx[b].cpu().numpy(), oB[b]), meta
+            assert bits_equal(R[b].cpu().numpy(), oR[b]), meta
+            ncand += len(oL[b])
+        npx += o.size
+    print(f"peaks sweep: {n} calls, {npx} pixels, {ncand} candidates")
+
+
 def test_peaks_large_random_vs_oracle():
     """128x128 maps with plateaus, saturation, every kernel shape; bit-exact."""
     H = W = 128
