@@ -566,7 +566,7 @@ class _DetectGraph:
 
 # the heads launch's image-major block order (an image's units innermost) for
 # up to this many units per image: config B (3 per image) 106.6 -> 106.0 ms
-# (profiles/r05c), config E (16 per image) 166.6 -> 168.5 ms (profiles/r05t).
+# (profiles/archive/r05/r05c), config E (16 per image) 166.6 -> 168.5 ms (profiles/archive/r05/r05t).
 # A/B knob TMR_HEADS_IMAGE_MAJOR_MAX (the flags field holds <= 255)
 HEADS_IMAGE_MAJOR_MAX = min(255, int(os.environ.get("TMR_HEADS_IMAGE_MAJOR_MAX", "4")))
 
@@ -576,7 +576,7 @@ class _no_gc:
     inside the capture can destroy an unreachable object that owns a HIP
     event or graph (an evicted replay's), and a destroy call during a global
     capture aborts the process (seen once in test_module_graph_replays_back_to_back,
-    profiles/r05aa).  torch.cuda.graph collects on entry; this keeps it off
+    profiles/archive/r05/r05aa).  torch.cuda.graph collects on entry; this keeps it off
     until the capture has ended."""
 
     def __enter__(self):
@@ -625,7 +625,7 @@ class TMREngine:
         # the two launches on two streams (subset launches: tmr_unit_t.out_unit).
         # "auto": only when images hold about one unit each -- with several
         # units per image the split loses the band staging they share
-        # (measured, profiles/r05b/xcorr_split_ab.json: config B 5.09 -> 5.38 ms,
+        # (measured, profiles/archive/r05/r05b/xcorr_split_ab.json: config B 5.09 -> 5.38 ms,
         # C 2.99 -> 3.56, E equal; D, one unit per image, 2.38 -> 2.19 ms)
         self.xcorr_split = "auto"
         self._side = None
@@ -641,7 +641,7 @@ class TMREngine:
         # ... or as the decoder's records themselves (no plane, no record pass):
         # off by default -- each block is one channel, so a record's 16 B come
         # from 8 blocks as 2-B stores: config C correlation 3.7 -> 8.0 ms, step
-        # 53.3 -> 56.7 ms against the plane + record pass (profiles/r05g)
+        # 53.3 -> 56.7 ms against the plane + record pass (profiles/archive/r05/r05g)
         self.out_records = os.environ.get("TMR_XCORR_RECORDS", "0") == "1"
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)

@@ -434,7 +434,7 @@ def test_graph_book_bounded_and_failures_remembered():
 def test_heads_image_major_only_for_few_units_per_image():
     """The heads launch runs image-major (an image's units innermost) up to
     HEADS_IMAGE_MAJOR_MAX units per image (config B's 3: faster; config E's
-    16: 1.1% slower, profiles/r05t), and only for units in image order."""
+    16: 1.1% slower, profiles/archive/r05/r05t), and only for units in image order."""
     from tmr_amd import engine
     upi = engine.TMREngine._units_per_image
     assert engine.HEADS_IMAGE_MAJOR_MAX == 4
