@@ -66,8 +66,12 @@ def py_nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> t
     if n == 0:
         return torch.zeros(0, dtype=torch.int64)
     x1, y1, x2, y2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
-    areas = (x2 - x1) * (y2 - y1)
-    order = np.argsort(-s, kind="stable")
+    with np.errstate(invalid="ignore", over="ignore"):
+        areas = (x2 - x1) * (y2 - y1)
+    # scores.sort(stable=true, descending=true): NaN of either sign first (torch
+    # orders NaN above +inf), -0.0 == +0.0, ties by index -- np.argsort(-s)
+    # would put NaN last
+    order = torch.sort(torch.from_numpy(s), stable=True, descending=True).indices.numpy()
     sup = np.zeros(n, bool)
     keep = []
     f = np.float32
@@ -80,11 +84,14 @@ def py_nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> t
             j = order[_j]
             if sup[j]:
                 continue
+            # Python's max(a, b) / min(a, b) pick like std::max(a, b) / std::min(a, b)
+            # (b only when b > a / b < a), NaN included
             xx1 = max(x1[i], x1[j]); yy1 = max(y1[i], y1[j])
             xx2 = min(x2[i], x2[j]); yy2 = min(y2[i], y2[j])
-            w = max(f(0), f(xx2 - xx1)); h = max(f(0), f(yy2 - yy1))
-            inter = f(w * h)
-            ovr = f(inter / f(f(areas[i] + areas[j]) - inter))
+            with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+                w = max(f(0), f(xx2 - xx1)); h = max(f(0), f(yy2 - yy1))
+                inter = f(w * h)
+                ovr = f(inter / f(f(areas[i] + areas[j]) - inter))
             if float(ovr) > float(iou_threshold):
                 sup[j] = True
     return torch.tensor(keep, dtype=torch.int64)
@@ -298,6 +305,122 @@ def gen_pred_boxes(R):
     return d
 
 
+PRED_BOX_EX_SIZES = {"full": (0.2, 0.25), "center": (1.0 / 48, 1.0 / 64), "vert": (1.0 / 48, 0.1),
+                     "horz": (0.1, 1.0 / 64), "cross": (2.5 / 24, 2.5 / 32)}
+
+
+def _store_pred_boxes(R, d, ci, meta, o, reg, ex, thr, box_reg, ab_b=False, ab_c=False):
+    batch = {"regression_ablation_b": ab_b, "regression_ablation_c": ab_c}
+    B = o.shape[0]
+    L, Bx, Rf = R.tu.Get_pred_boxes([o], [reg] if box_reg else [None], ex, batch, thr, box_reg)
+    probs = np.stack([o[b].sigmoid().squeeze(0).numpy() for b in range(B)])
+    meta = dict(meta, thr=thr, box_reg=box_reg, ab_b=ab_b, ab_c=ab_c)
+    d[f"c{ci}_meta"] = np.array(json.dumps(meta))
+    d[f"c{ci}_o"] = o.numpy(); d[f"c{ci}_reg"] = reg.numpy()
+    d[f"c{ci}_prob"] = probs
+    d[f"c{ci}_ex"] = np.stack([e[0].numpy() for e in ex])
+    d.update(_flatten_lists(f"c{ci}_logits", L))
+    d.update(_flatten_lists(f"c{ci}_boxes", Bx))
+    d.update(_flatten_lists(f"c{ci}_refs", Rf))
+
+
+def gen_pred_boxes_nonfinite(R):
+    """Get_pred_boxes on maps holding NaN / +-inf (TM_utils.py:246-254, 359):
+    torch.max over the masked taps propagates NaN, so a pixel with a NaN
+    anywhere in its masked window is never a peak.  Per adaptive kernel shape:
+    a would-be peak with a NaN at the FIRST masked tap, one with a NaN at the
+    LAST masked tap, a NaN centre, a plateau with a NaN beside it, +inf logits
+    (p = 1.0, a saturated pair), -inf logits (p = 0), a NaN regression value
+    at a peak; then an all-NaN image (dummy row) and a map sprinkled with
+    NaN / +-inf."""
+    B, H, W = 3, 24, 32
+    d = {}
+    ci = 0
+    for kname, (eh, ew) in PRED_BOX_EX_SIZES.items():
+        taps = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
+        mask = oracle.adaptive_kernel(np.float32(eh), np.float32(ew), H, W)
+        on = [t for t, m in zip(taps, mask.ravel()) if m]
+        for thr, box_reg in ((0.1, True), (0.5, True), (0.25, False)):
+            o = torch.from_numpy((synth.normal(1500 + ci, (B, 1, H, W)) * 0.5 - 2.0).astype(np.float32))
+            reg = torch.from_numpy((synth.normal(1600 + ci, (B, 4, H, W)) * 0.3).astype(np.float32))
+            m = o[0, 0]
+            nan = float("nan")
+            # a would-be peak, NaN at the first masked tap (row-major), and at the last
+            m[4, 4] = 3.0; m[4 + on[0][0], 4 + on[0][1]] = nan
+            m[4, 12] = 3.0; m[4 + on[-1][0], 12 + on[-1][1]] = nan
+            m[4, 20] = 3.0                       # a clean peak for comparison
+            m[10, 5] = nan                       # NaN centre
+            m[10:12, 12:15] = 2.0; m[10, 15] = nan   # plateau, NaN beside its right end
+            m[16, 3] = float("inf"); m[16, 4] = float("inf")   # saturated p = 1.0 pair
+            m[16, 10] = float("inf")             # lone +inf
+            m[15:18, 19:22] = 1.0; m[16, 20] = float("-inf")   # -inf inside a ring of equal peaks
+            m[20, 28] = 2.5                      # a peak whose regression holds NaN
+            reg[0, 2, 20, 28] = nan
+            m[0, 0] = nan; m[0, 1] = 2.0         # NaN in the zero-padded corner's window
+            m[H - 1, W - 1] = 4.0; m[H - 2, W - 2] = nan
+            o[1] = nan                           # every pixel NaN: the dummy row
+            flat = o[2].view(-1)
+            u = synth.uniform(1700 + ci, 3 * 40)
+            for j in range(40):
+                flat[int(u[3 * j] * flat.numel()) % flat.numel()] = [nan, float("inf"), float("-inf")][
+                    int(u[3 * j + 1] * 3) % 3]
+                flat[int(u[3 * j + 2] * flat.numel()) % flat.numel()] = 1.5
+            ex = []
+            for b in range(B):
+                x1, y1 = 0.1 + 0.05 * b, 0.2
+                ex.append(torch.tensor([[x1, y1, x1 + ew, y1 + eh]], dtype=torch.float32))
+            _store_pred_boxes(R, d, ci, dict(kernel=kname), o, reg, ex, thr, box_reg)
+            ci += 1
+    d["n"] = np.array(ci)
+    return d
+
+
+def gen_nms_nonfinite(R):
+    """NMS with non-finite inputs (TM_utils.py:307-323 -> torchvision nms):
+    NaN scores of both signs sort first (torch.sort descending), +-inf
+    scores, -0.0 / +0.0 ties, NaN / inf box coordinates (a NaN area gives a
+    NaN IoU: never suppresses, never suppressed); small sets (one-workgroup
+    path) and sets over 256 rows (the binned path)."""
+    d = {}
+    cases = []
+    qn = np.array([0xffc00000], np.uint32).view(np.float32)[0]   # x86's default NaN (negative)
+    b = np.array([[0, 0, 1, 1], [0.1, 0, 1.1, 1], [0, 0.1, 1, 1.1], [0.05, 0.05, 1, 1],
+                  [2, 2, 3, 3], [2.1, 2, 3.1, 3], [0, 0, 1, 1], [5, 5, 6, 6]], np.float32)
+    s = np.array([0.5, np.nan, 0.9, np.inf, 0.0, -0.0, qn, -np.inf], np.float32)
+    cases += [(b, s, 0.5), (b, s, 0.15), (b, s, -0.1)]
+    s2 = np.array([-0.0, 0.0, -0.0, 0.0, 0.7, 0.7, np.nan, np.nan], np.float32)
+    cases.append((b, s2, 0.3))
+    b3 = b.copy(); b3[1, 0] = np.nan; b3[3, 2] = np.inf; b3[5] = [np.inf, np.inf, np.inf, np.inf]
+    b3[4, 1] = -np.inf
+    s3 = np.array([0.9, 0.95, 0.8, 0.85, 0.6, 0.6, 0.5, 0.4], np.float32)
+    cases += [(b3, s3, 0.5), (b3, s, 0.15)]
+    for i, n in enumerate((40, 300, 700)):
+        u = synth.uniform(1900 + i, 6 * n).reshape(n, 6).astype(np.float32)
+        xy = u[:, :2] * 0.6
+        bx = np.concatenate([xy, xy + 0.05 + u[:, 2:4] * 0.2], 1).astype(np.float32)
+        sc = (np.round(u[:, 4] * 8) / 8).astype(np.float32)
+        pick = u[:, 5]
+        sc[pick < 0.05] = np.nan
+        sc[(pick >= 0.05) & (pick < 0.08)] = qn
+        sc[(pick >= 0.08) & (pick < 0.1)] = np.inf
+        sc[(pick >= 0.1) & (pick < 0.12)] = -np.inf
+        sc[(pick >= 0.12) & (pick < 0.15)] = -0.0
+        bx[(pick >= 0.15) & (pick < 0.17), 2] = np.nan
+        bx[(pick >= 0.17) & (pick < 0.18), 3] = np.inf
+        cases.append((bx, sc, [0.5, 0.15, 0.65][i]))
+    for i, (bx, sc, thr) in enumerate(cases):
+        logits = [torch.from_numpy(np.stack([sc, np.zeros_like(sc)], 1))]
+        boxes = [torch.from_numpy(bx.copy())]
+        refs = [torch.from_numpy(bx[:, :2].copy())]
+        L, Bx, Rf = R.tu.NMS(logits, boxes, refs, thr)
+        keep = py_nms(torch.from_numpy(bx), torch.from_numpy(sc), thr).numpy()
+        d[f"c{i}_boxes"] = bx; d[f"c{i}_scores"] = sc; d[f"c{i}_thr"] = np.array(thr)
+        d[f"c{i}_keep"] = keep; d[f"c{i}_kept_boxes"] = Bx[0].numpy()
+        d[f"c{i}_kept_logits"] = L[0].numpy()
+    d["n"] = np.array(len(cases))
+    return d
+
+
 def gen_nms(R):
     d = {}
     cases = []
@@ -364,6 +487,7 @@ def gen_caller(R):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--only", nargs="*", help="regenerate only these fixtures (names without .npz)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     torch.set_num_threads(8)
@@ -373,10 +497,14 @@ def main():
                 stubs="roi_align=oracle C restatement (unpinned); nms=py_nms transcription (unpinned)")
     jobs = {"xcorr": lambda: gen_xcorr(R), "template": lambda: gen_template(R),
             "pred_boxes": lambda: gen_pred_boxes(R), "nms": lambda: gen_nms(R),
-            "caller": lambda: gen_caller(R)}
+            "caller": lambda: gen_caller(R),
+            "pred_boxes_nonfinite": lambda: gen_pred_boxes_nonfinite(R),
+            "nms_nonfinite": lambda: gen_nms_nonfinite(R)}
     for name, kw in FORWARD_VARIANTS.items():
         jobs[f"forward_{name}"] = (lambda kw=kw, name=name: gen_forward(R, name, kw))
     for name, fn in jobs.items():
+        if a.only and name not in a.only:
+            continue
         d = fn()
         d["meta"] = np.array(json.dumps(meta))
         np.savez_compressed(os.path.join(a.out, f"{name}.npz"), **d)

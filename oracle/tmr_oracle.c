@@ -272,16 +272,20 @@ int64_t orc_peaks_decode(const float *p, const float *reg, int H, int W,
         for (int x = 0; x < W; ++x) {
             float v = p[y * W + x];
             if (!(v >= thr)) continue;
+            /* pooled = selected_positions.max(dim=2) (:359): torch.max propagates
+             * NaN, so a NaN anywhere among the masked taps makes pooled NaN and
+             * `pooled == p` (:253) False -- the pixel is never a peak. */
             float mx = -INFINITY;
-            int first = 1;
+            int first = 1, nan = 0;
             for (int dy = -1; dy <= 1; ++dy)
                 for (int dx = -1; dx <= 1; ++dx) {
                     if (!mask[(dy + 1) * 3 + dx + 1]) continue;
                     int yy = y + dy, xx = x + dx;
                     float q = (yy < 0 || yy >= H || xx < 0 || xx >= W) ? 0.0f : p[yy * W + xx];
+                    if (q != q) nan = 1;
                     if (first || q > mx) { mx = q; first = 0; }
                 }
-            if (!(mx == v)) continue;
+            if (nan || !(mx == v)) continue;
             if (n < cap) {
                 int64_t i = n;
                 if (idx) idx[i] = (int64_t)y * W + x;
@@ -314,11 +318,17 @@ int64_t orc_peaks_decode(const float *p, const float *reg, int H, int W,
  * stable descending sort on score, IoU in fp32, compared in double.
  * ------------------------------------------------------------------------ */
 static const float *g_sort_scores;
+/* scores.sort(stable=true, descending=true): torch orders NaN (either sign)
+ * above +inf, all NaNs equal; -0.0 == +0.0; ties keep the lower index. */
 static int cmp_desc_stable(const void *a, const void *b) {
     int64_t i = *(const int64_t *)a, j = *(const int64_t *)b;
     float si = g_sort_scores[i], sj = g_sort_scores[j];
-    if (si > sj) return -1;
-    if (si < sj) return 1;
+    int ni = si != si, nj = sj != sj;
+    if (ni != nj) return ni ? -1 : 1;
+    if (!ni) {
+        if (si > sj) return -1;
+        if (si < sj) return 1;
+    }
     return (i < j) ? -1 : (i > j);
 }
 
@@ -344,12 +354,14 @@ int64_t orc_nms(const float *boxes, const float *scores, int64_t n, double thr, 
             int64_t j = order[_j];
             if (sup[j]) continue;
             const float *bj = boxes + 4 * j;
-            float xx1 = bi[0] > bj[0] ? bi[0] : bj[0];
-            float yy1 = bi[1] > bj[1] ? bi[1] : bj[1];
-            float xx2 = bi[2] < bj[2] ? bi[2] : bj[2];
-            float yy2 = bi[3] < bj[3] ? bi[3] : bj[3];
-            float w = xx2 - xx1; if (!(w > 0.0f)) w = 0.0f;
-            float h = yy2 - yy1; if (!(h > 0.0f)) h = 0.0f;
+            /* std::max(ix1, x1[j]) = ix1 < x1[j] ? x1[j] : ix1, std::min likewise
+             * (a NaN coordinate makes an area NaN, so ovr is NaN and never > thr) */
+            float xx1 = bi[0] < bj[0] ? bj[0] : bi[0];
+            float yy1 = bi[1] < bj[1] ? bj[1] : bi[1];
+            float xx2 = bj[2] < bi[2] ? bj[2] : bi[2];
+            float yy2 = bj[3] < bi[3] ? bj[3] : bi[3];
+            float w = xx2 - xx1; if (!(0.0f < w)) w = 0.0f;
+            float h = yy2 - yy1; if (!(0.0f < h)) h = 0.0f;
             float inter = w * h;
             float ovr = inter / (areas[i] + areas[j] - inter);
             if ((double)ovr > thr) sup[j] = 1;

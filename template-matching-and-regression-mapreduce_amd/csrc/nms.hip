@@ -121,9 +121,15 @@ inline int64_t work_bytes(int64_t T, int64_t sum_nb, int G) {
     return (int64_t)(w.temp - (char *)nullptr) + w.temp_bytes + 256;
 }
 
+// Ascending float order as torch.sort compares (descending = its complement):
+// -0.0 == +0.0, and every NaN, of either sign and any payload, above +inf and
+// equal to each other -- so the stable descending sort puts NaN scores first
+// in index order, as scores.sort(stable=True, descending=True) in
+// torchvision's nms_kernel.cpp does.
 __device__ __forceinline__ uint32_t radix_key(float f) {
     uint32_t b = __float_as_uint(f);
-    if (b == 0x80000000u) b = 0u;  // rocprim's digit extractor: -0.0 sorts as +0.0
+    if (f != f) return 0xffffffffu;
+    if (b == 0x80000000u) b = 0u;
     return b ^ ((b & 0x80000000u) ? 0xffffffffu : 0x80000000u);
 }
 

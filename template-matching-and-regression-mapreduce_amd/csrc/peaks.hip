@@ -69,8 +69,8 @@ __global__ void maxpool3x3_kernel(const float *__restrict__ x, int64_t n, int H,
 
 // The probability map, chip-wide (one thread per 4 pixels): p = sigmoid(o)
 // (near-correctly rounded), or o itself when the input is already p.  With
-// TMR_PEAKS_PROB_SCRATCH the caller does not want the map: a logit below
-// logit(thr) by a 1e-3 relative margin is written as -1 without its sigmoid
+// TMR_PEAKS_PROB_SCRATCH the caller does not want the map: a logit whose
+// sigmoid cannot round to thr or above is written as -1 without its sigmoid
 // -- it can neither be a candidate nor beat one (its p < thr <= the
 // candidate's p) -- and NaN stays NaN.  (Computing the sigmoid inside the
 // one-workgroup-per-unit finder left a single unit's map to one CU: 25 us
@@ -94,9 +94,14 @@ __global__ __launch_bounds__(256) void prob_kernel(const float *__restrict__ o, 
                 const float thr = params[u].thr;
                 olo = -INFINITY;
                 if (thr > 0.0f) {
-                    const double t = (double)thr;
-                    const double lg = t < 1.0 ? log(t / (1.0 - t)) : 15.0;
-                    olo = (float)(lg - 1e-3 * (1.0 + fabs(lg)));
+                    // p = (float)sigmoid(x) reaches thr only when the exact sigmoid is at least
+                    // the midpoint between thr and the float below it; a logit under that
+                    // midpoint's logit (less a margin far above the double sigmoid's error and
+                    // olo's own fp32 rounding) cannot round up to thr, even for thr near 1
+                    const float tq = fminf(thr, 1.0f);
+                    const double mid = 0.5 * ((double)tq + (double)nextafterf(tq, 0.0f));
+                    const double lg = log(mid / (1.0 - mid));
+                    olo = (float)(lg - 1e-5 * (1.0 + fabs(lg)));
                 }
             }
             v = x < olo ? -1.0f : tmr_sigmoid_cr(x);
@@ -156,8 +161,8 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ pm
             if (i < np) {
                 const int ly = (int)(((float)i + 0.5f) * rW) + 1, x = i - (ly - 1) * W;
                 const float v = sp[ly * W + x];
-                if (v >= pp.thr) {  // masked 3x3 max (TM_utils.py:337-361): first tap, then strict >
-                    float mx = 0.0f;
+                if (v >= pp.thr) {  // masked 3x3 max (TM_utils.py:337-361): first tap, then strict >;
+                    float mx = 0.0f;  // a NaN tap sticks (torch.max, :359), so `pooled == p` (:253) fails
                     bool first = true;
 #pragma unroll
                     for (int dy = -1; dy <= 1; ++dy)
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(PNT) void peaks_kernel(const float *__restrict__ pm
                             if (!((pp.mask >> ((dy + 1) * 3 + dx + 1)) & 1)) continue;
                             const int xx = x + dx;
                             const float q = (xx < 0 || xx >= W) ? 0.0f : sp[(ly + dy) * W + xx];
-                            if (first || q > mx) { mx = q; first = false; }
+                            if (first || q > mx || q != q) { mx = q; first = false; }
                         }
                     f = mx == v;
                 }

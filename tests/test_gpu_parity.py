@@ -52,6 +52,17 @@ def bits_equal(a, b):
     return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def bits_equal_nan(a, b):
+    """bits_equal, except that a NaN matches any NaN (the payload of a NaN
+    that propagates through exp / products is not part of the contract)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    if a.shape != b.shape or not np.array_equal(np.isnan(a), np.isnan(b)):
+        return False
+    m = ~np.isnan(b)
+    return np.array_equal(a[m].view(np.uint32), b[m].view(np.uint32))
+
+
 # ----------------------------------------------------------------- templates
 def test_roi_align_bitexact_vs_oracle(golden):
     g = golden("template")
@@ -521,10 +532,15 @@ def test_custom_shape_maxpool_vs_reference(shape):
         tmr_amd.custom_shape_3x3_maxpool2d(x.to(DEV), [[0] * 3] * 3)
 
 
-def test_get_pred_boxes_golden(golden):
+@pytest.mark.parametrize("name", ["pred_boxes", "pred_boxes_nonfinite"])
+def test_get_pred_boxes_golden(golden, name):
     """Bit-exact given identical score maps: feed the reference's own
-    sigmoid output (input_is_prob) and compare every candidate."""
-    g = golden("pred_boxes")
+    sigmoid output (input_is_prob) and compare every candidate.  The
+    _nonfinite fixture holds NaN at the first / last masked tap of would-be
+    peaks, NaN centres, NaN beside plateaus, +-inf logits, a NaN regression
+    value and an all-NaN map: the reference's torch.max propagates NaN
+    (TM_utils.py:253,359), so no pixel with a NaN in its window is a peak."""
+    g = golden(name)
     for i in range(int(g["n"])):
         meta = json.loads(str(g[f"c{i}_meta"]))
         prob, reg, ex = g[f"c{i}_prob"], g[f"c{i}_reg"], g[f"c{i}_ex"]
@@ -541,8 +557,22 @@ def test_get_pred_boxes_golden(golden):
             l, bx, r = L[b].cpu().numpy(), Bx[b].cpu().numpy(), R[b].cpu().numpy()
             assert bits_equal(l, gL[b]), (i, b, meta)
             assert bits_equal(r, gR[b]), (i, b)
-            assert bits_equal(bx, gB[b]), (i, b)  # the reference's own decode, bit for bit
-            assert bits_equal(bx, oB[b]), (i, b)
+            assert bits_equal_nan(bx, gB[b]), (i, b)  # the reference's own decode, bit for bit
+            assert bits_equal_nan(bx, oB[b]), (i, b)
+        if name == "pred_boxes_nonfinite":
+            # from the logits, the probability map discarded (the kernel's scratch
+            # mode, detect's and Get_pred_boxes' default): the same candidates as the
+            # oracle on the path's sigmoid of those logits
+            o = g[f"c{i}_o"]
+            L2, B2, R2 = tmr_amd.Get_pred_boxes([cuda(o)], regs, exl, batch, meta["thr"], meta["box_reg"])
+            pl = oracle.sigmoid_cr(o[:, 0])
+            qL, qB, qR = oracle.get_pred_boxes_prob(list(pl), list(reg) if meta["box_reg"] else None,
+                                                    [e[None] for e in ex], meta["thr"], meta["box_reg"],
+                                                    meta["ab_b"], meta["ab_c"])
+            for b in range(len(qL)):
+                assert bits_equal(L2[b].cpu().numpy(), qL[b]), (i, b, meta)
+                assert bits_equal_nan(B2[b].cpu().numpy(), qB[b]), (i, b)
+                assert bits_equal(R2[b].cpu().numpy(), qR[b]), (i, b)
 
 
 def test_get_pred_boxes_empty_units_dummy_row():
@@ -604,6 +634,11 @@ def _peaks_sweep_case(r):
     boxes = np.stack([x1, y1, x1 + bw, y1 + bh], 1).astype(np.float32)
     thr = float(r.uniform(0.01, 0.99))
     box_reg = bool(r.random() < 0.8)
+    if r.random() < 0.1:  # thresholds near 1: logits across the band that rounds to thr
+        thr = float(np.float32(1.0 - 10.0 ** -r.uniform(3.0, 7.2)))
+        lg = np.log(thr / (1.0 - thr))
+        sel = r.random(flat.size) < 0.3
+        flat[sel] = (lg + r.uniform(-1.0, 1.0, int(sel.sum()))).astype(np.float32)
     ab = int(r.integers(0, 4))  # 0, 1: none; 2: ablation_b; 3: ablation_c
     return o, reg, boxes, thr, box_reg, ab == 2, ab == 3
 
@@ -659,8 +694,13 @@ def test_peaks_large_random_vs_oracle():
 
 
 # ----------------------------------------------------------------- nms
-def test_nms_golden(golden):
-    g = golden("nms")
+@pytest.mark.parametrize("name", ["nms", "nms_nonfinite"])
+def test_nms_golden(golden, name):
+    """Keep lists and kept rows vs the reference's NMS.  _nonfinite: NaN
+    scores of either sign sort first (torch.sort descending, stable), +-inf
+    scores, -0.0 == +0.0 ties, NaN / inf coordinates; 8-row sets (one
+    workgroup) and 300 / 700-row sets (radix sort + binned pairs)."""
+    g = golden(name)
     for i in range(int(g["n"])):
         bx, sc, thr = g[f"c{i}_boxes"], g[f"c{i}_scores"], float(g[f"c{i}_thr"])
         keep = tmr_amd.NMS_process(cuda(bx), cuda(np.stack([sc, np.zeros_like(sc)], 1)), thr)
@@ -669,6 +709,8 @@ def test_nms_golden(golden):
             L, B, R = tmr_amd.NMS([cuda(np.stack([sc, np.zeros_like(sc)], 1))], [cuda(bx)],
                                   [cuda(bx[:, :2].copy())], thr)
             assert bits_equal(B[0].cpu().numpy(), g[f"c{i}_kept_boxes"]), i
+            if f"c{i}_kept_logits" in g:
+                assert bits_equal(L[0].cpu().numpy(), g[f"c{i}_kept_logits"]), i
 
 
 @pytest.mark.parametrize("n,thr", [(1, 0.5), (63, 0.5), (64, 0.15), (65, 0.5), (700, 0.5),
@@ -695,7 +737,7 @@ def test_nms_small_images_one_workgroup_path():
     kernel; a call with a larger image runs gather + radix sort + strips for
     every image.  The same image gives the same kept rows and order either
     way -- ties, duplicate boxes, zero-area boxes, -0.0 / +0.0 and NaN
-    scores included -- and equals the oracle where it is defined (no NaN)."""
+    scores included -- and equals the oracle (NaN scores sort first)."""
     big_bx, big_sc = _nms_case(501, 900)
     for seed, n in ((502, 1), (503, 17), (504, 64), (505, 65), (506, 200), (507, 256)):
         bx, sc = _nms_case(seed, n)
@@ -716,9 +758,8 @@ def test_nms_small_images_one_workgroup_path():
                 assert bits_equal(L1[0].cpu().numpy(), L2[0].cpu().numpy()), (n, with_nan, thr)
                 assert bits_equal(B1[0].cpu().numpy(), B2[0].cpu().numpy()), (n, with_nan, thr)
                 assert bits_equal(R1[0].cpu().numpy(), R2[0].cpu().numpy()), (n, with_nan, thr)
-                if not with_nan:
-                    keep = oracle.nms(bx, s2, thr)
-                    assert bits_equal(B1[0].cpu().numpy(), bx[keep]), (n, thr)
+                keep = oracle.nms(bx, s2, thr)  # NaN scores first, as torch.sort(descending)
+                assert bits_equal(B1[0].cpu().numpy(), bx[keep]), (n, with_nan, thr)
 
 
 def _nms_binned_cases():
@@ -1249,7 +1290,7 @@ def test_xcorr_mfma_lds_fragments_bitexact(prec, H, W, kmax):
         assert bits_equal(res["lds"][t], res["split"][t]), (prec, t)
 
 
-@pytest.mark.parametrize("thr", [0.1, 0.5, 0.999, 1.0, 0.0])
+@pytest.mark.parametrize("thr", [0.1, 0.5, 0.999, 0.9999999, 0.99999994, 1.0, 0.0, 1e-30])
 def test_peaks_without_prob_match_with_prob(thr):
     """TMREngine.peaks without the probability map (detect, Get_pred_boxes)
     stages a logit well below the threshold's as -1 instead of its sigmoid:
@@ -1266,6 +1307,10 @@ def test_peaks_without_prob_match_with_prob(thr):
             near = np.nextafter(np.full(40, lg, np.float32), away)
             o[0, 0, 5, :40] = near
             o[1, 0, 7, 3:43] = lg
+            # a sweep across the band of logits whose sigmoid ROUNDS to thr (near 1 that
+            # band is far wider than ulps of the logit: ADVICE r5)
+            o[4, 0, 2, :64] = np.linspace(lg - 0.7, lg + 0.7, 64, dtype=np.float32)
+            o[4, 0, 4, :64] = np.linspace(lg - 0.7, lg + 0.7, 64, dtype=np.float32)[::-1]
         o[2, 0, 3, 4] = np.nan
         o[2, 0, 9, 9] = np.inf
         o[2, 0, 11, 2] = -np.inf

@@ -29,8 +29,12 @@ def corner_ok(a, b):
         return False
     if a.size == 0:
         return True
-    scale = np.spacing(np.abs(b).max(axis=-1, keepdims=True).astype(np.float32))
-    return bool((np.abs(a.astype(np.float64) - b) <= 2 * scale).all())
+    if not np.array_equal(np.isnan(a), np.isnan(b)):
+        return False
+    ok = np.isnan(b) | (a == b)  # NaN where the reference has NaN (a NaN regression), inf alike
+    scale = np.spacing(np.nanmax(np.abs(np.where(np.isfinite(b), b, 0)), axis=-1, keepdims=True).astype(np.float32))
+    with np.errstate(invalid="ignore"):
+        return bool((ok | (np.abs(a.astype(np.float64) - b) <= 2 * scale)).all())
 
 
 def ulp_diff(a, b):
@@ -107,8 +111,12 @@ def _split(g, key):
     return out
 
 
-def test_pred_boxes(golden):
-    g = golden("pred_boxes")
+@pytest.mark.parametrize("name", ["pred_boxes", "pred_boxes_nonfinite"])
+def test_pred_boxes(golden, name):
+    """Every candidate bit-exact vs the reference's Get_pred_boxes; the
+    _nonfinite fixture pins NaN / +-inf maps (torch.max's NaN propagation
+    through the masked 3x3 window, TM_utils.py:253,359)."""
+    g = golden(name)
     max_ulp = 0
     for i in range(int(g["n"])):
         meta = json.loads(str(g[f"c{i}_meta"]))
@@ -134,11 +142,17 @@ def test_pred_boxes(golden):
     print("correctly rounded exp instead: max corner ulp diff vs reference:", max_ulp)
 
 
-def test_nms(golden):
-    g = golden("nms")
+@pytest.mark.parametrize("name", ["nms", "nms_nonfinite"])
+def test_nms(golden, name):
+    """Keep lists vs the reference's NMS (through the nms transcription; the
+    _nonfinite fixture: NaN scores first as torch.sort(descending) puts them,
+    +-inf, -0.0 == +0.0, NaN / inf coordinates)."""
+    g = golden(name)
     for i in range(int(g["n"])):
         keep = oracle.nms(g[f"c{i}_boxes"], g[f"c{i}_scores"], float(g[f"c{i}_thr"]))
         assert np.array_equal(keep, g[f"c{i}_keep"]), i
+        if f"c{i}_kept_boxes" in g and g[f"c{i}_boxes"].shape[0]:
+            assert np.array_equal(g[f"c{i}_boxes"][keep], g[f"c{i}_kept_boxes"], equal_nan=True), i
 
 
 def test_caller_sequence(golden):
