@@ -285,9 +285,6 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="initialise torch.distributed and run the reducer exchange even at one rank "
                          "(RCCL at world 1 on a 1-GPU box exercises the N>1 code path)")
-    ap.add_argument("--xcorr-split", type=int, default=None, choices=(0, 1),
-                    help="correlation of a mixed launch split by kernel per unit on two streams "
-                         "(TMREngine.xcorr_split; default: the engine's)")
     ap.add_argument("--no-xcorr-classes", action="store_true",
                     help="skip the per-template-class correlation launches after the timed region "
                          "(PMC passes: one launch per kernel role)")
@@ -370,8 +367,6 @@ def main():
     # per-kernel events, so the kernels' HIP-event times then come from one
     # eager step after the timed loop (same kernels, same stream)
     eng.use_graphs = not a.no_graphs
-    if a.xcorr_split is not None:
-        eng.xcorr_split = bool(a.xcorr_split)
     if a.path == "module":  # the module's engine replays each exemplar's forward
         model.engine().use_graphs = not a.no_graphs
     graphs = eng.use_graphs and (a.path == "module" or B * E <= eng.GRAPH_MAX_UNITS)
@@ -417,11 +412,11 @@ def main():
         algo = eng.last_decoder_algo
         terms = SPLIT_TERMS[prec]
         peak = F16_PEAK_TFLOPS
-        kernel_name = ("tmr_split_conv_heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
+        kernel_name = ("tmr_split_conv heads (direct implicit-GEMM decoder_b+decoder_o f_TM half "
                        "+ LeakyReLU + 1x1 heads, v_mfma_f32_16x16x32_%s)"
                        % ("bf16" if prec == "bf16" else "f16"))
         flops_basis = ("executed 16-bit MFMA work: %d term(s) x 2*H*W*N(2048)*K(512*9) per unit "
-                       "(%s; the fp half runs once per image in tmr_split_conv_store and is "
+                       "(%s; the fp half runs once per image in a tmr_split_conv store launch and is "
                        "shared by its exemplars; unshared (E=1): K=(256+512)*9, the fp half folded through input_proj)"
                        % (terms, "fp32-grade 3-term fp16 split: hi*hi + lo*hi + hi*lo"
                           if terms == 3 else "one %s term" % prec))
@@ -504,15 +499,12 @@ def main():
         xs = float(np.mean(xc_ms)) / 1e3
         xk = eng.last_xcorr_algo
         out["roofline_xcorr"] = {
-            "kernel": ("tmr_xcorr_prec MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
+            "kernel": ("tmr_xcorr MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
                        + ("v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if prec == "fp32" else
                           "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
                                                                      else ("f16", "scaled fp16")))
                        if xk == "mfma" else
-                       "tmr_xcorr_out split per unit: VALU (xcorr_rows_kernel) for the units the per-k cost "
-                       "model gives it, MFMA (xcorr_mfma_kernel, row-Toeplitz) for the rest, two streams"
-                       if xk == "split" else
-                       "tmr_xcorr_prec VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
+                       "tmr_xcorr VALU (xcorr_rows_kernel: LDS-blocked v_pk_fma_f32)")
                       + " + /hw + pad + scale + max|f_TM|; kernel chosen by the measured per-k cost model "
                         "(engine.XCORR_COST)",
             "algo": xk,

@@ -30,7 +30,10 @@
 extern "C" {
 #endif
 
-#define TMR_ABI_VERSION 2  /* 2: per-unit out_absmax, per-sample activation scales */
+#define TMR_ABI_VERSION 3  /* 2: per-unit out_absmax, per-sample activation scales;
+                            * 3: one correlation entry point (tmr_xcorr_args_t), one
+                            * sizing query (tmr_size), one split conv entry point,
+                            * no subset launches (tmr_unit_t.out_unit removed) */
 
 enum {
     TMR_OK = 0,
@@ -50,12 +53,10 @@ typedef struct tmr_unit {
     float roi[4];          /* roi_align box in feature px (x1,y1,x2,y2), :61-63   */
     int32_t pbox[4];       /* prototype snapped box (x1,y1,x2,y2), :49-50         */
     int64_t tmpl_offset;   /* float offset of this unit's [C,ht,wt] template      */
-    int32_t row_offset;    /* sum of ht over the units before this one (the MFMA  */
-                           /* correlation's split-template rows, tmr_template_split) */
-    int32_t out_unit;      /* the correlation's output plane [out_unit][C][H][W], */
-                           /* out_absmax slot and split-template exponent row: the */
-                           /* unit's index in the full unit set (= its position,   */
-                           /* unless a launch covers a subset of the units)        */
+    int32_t row_offset;    /* sum of ht * tsplit_nk(wt) over the units before this */
+                           /* one (the MFMA correlation's split-template rows,    */
+                           /* tmr_template_split)                                  */
+    int32_t pad_;
 } tmr_unit_t;
 
 /* Per-unit peak-finder parameters (utils/TM_utils.py:236-278). */
@@ -69,6 +70,29 @@ typedef struct tmr_peak_param {
 
 int tmr_version(void);
 const char *tmr_strerror(int rc);
+
+/* ---- sizes of the caller-provided buffers ---------------------------------
+ * tmr_size(kind, d0..d5) returns the size of a buffer the caller allocates
+ * (bytes, or floats where noted), or -1 for invalid dimensions; unused
+ * dimensions are 0.
+ *   TMR_SIZE_TEMPLATE_SPLIT (U, C, total_rows)          bytes, tmr_template_split
+ *   TMR_SIZE_HEADS_PARTIALS (N, U, H, W)                floats, tmr_split_conv heads
+ *   TMR_SIZE_XPACK          (S, C, H, W, ks, prec)      bytes, tmr_split_xpack (H, W at
+ *                                                       the output resolution)
+ *   TMR_SIZE_WPACK          (N, C0, C1, ks, prec)       bytes, tmr_split_wpack
+ *   TMR_SIZE_ACC            (U, N, H, W)                floats, TMR_SPLIT_TILED_OUT slabs
+ *   TMR_SIZE_NMS_WORK       (total_cand, sum_nb, max_cand, G)  bytes, tmr_nms
+ *   TMR_SIZE_STATS_WORK     (B)                         bytes, tmr_feature_stats */
+enum {
+    TMR_SIZE_TEMPLATE_SPLIT = 1,
+    TMR_SIZE_HEADS_PARTIALS = 2,
+    TMR_SIZE_XPACK = 3,
+    TMR_SIZE_WPACK = 4,
+    TMR_SIZE_ACC = 5,
+    TMR_SIZE_NMS_WORK = 6,
+    TMR_SIZE_STATS_WORK = 7
+};
+int64_t tmr_size(int kind, int64_t d0, int64_t d1, int64_t d2, int64_t d3, int64_t d4, int64_t d5);
 
 /* ---- (a2+a13) bilinear x2 upsample ---------------------------------------
  * f[0] = F.interpolate(feat, scale_factor=2, mode='bilinear',
@@ -86,70 +110,53 @@ int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *
 
 /* ---- (a9+a4) depthwise cross-correlation + pad + scale -------------------
  * out[u] = pad(conv2d(f[img(u)], T_u, groups=C) / fl32(ht*wt)) * scale
- * (models/template_matching.py:23-41, :97).  scale is a device scalar.
- * Units must be sorted by image; img_units (device int32[B+1]) gives each
- * image's unit range, so the image's feature plane is staged once for all of
- * its exemplars.
- * squeeze!=0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and
- * `work` must hold U*C*H*W floats; otherwise out is [U,C,H,W] and work may
- * be NULL.  relu_out (nullable) receives relu(out) (matching_net.py:79).
- * out_absmax (nullable, device float[U], zeroed by the caller): the kernel
- * raises out_absmax[u] to max |out[u]| (one atomic per workgroup and unit),
- * the split decoder's PER-UNIT activation scale source (tmr_split_xpack with
- * xmax_per_sample, TMR_SPLIT_XMAX_PER_UNIT), with no extra pass over out. */
-int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
-              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
-              const float *scale, int squeeze, float *out, float *relu_out, float *work,
-              float *out_absmax, void *stream);
-/* Same operation with the kernel chosen explicitly: TMR_XCORR_VALU (fp32
- * LDS-blocked wavefront kernels), TMR_XCORR_MFMA (row-Toeplitz implicit GEMM
- * on v_mfma_f32_16x16x32_f16 with the fp32-grade 3-term split: W % 32 == 0,
- * W <= 256, templates <= 31x31; TMR_E_UNSUPPORTED otherwise) or
- * TMR_XCORR_AUTO (MFMA when the shape fits it and min_k -- the smallest
- * template side in the launch -- reaches the counter-chosen crossover,
- * DESIGN.md §4.3; VALU otherwise).  tmpl_split (nullable) holds
- * tmr_template_split(templates, ..., total_rows, ...) of the same templates:
- * the MFMA kernel then loads its A fragments from it; NULL (TMR_PREC_F16X3
- * only, else TMR_E_UNSUPPORTED): the kernel builds the same fragments from
- * the templates itself (staged in LDS per unit and channel; bit-identical
- * results).  tmr_xcorr(...) runs the VALU kernels. */
+ * (models/template_matching.py:23-41, :97), one launch over all units:
+ *  f [B,C,H,W] (the projected features fp); templates from tmr_templates;
+ *  units [U] sorted by image, img_units (device int32[B+1]) each image's unit
+ *  range (an image's feature band is staged once for all of its exemplars);
+ *  scale: device scalar (matcher.scale).
+ *  squeeze != 0: out is [U,1,H,W] = pad(sum_c ...) * scale (:34-35) and `work`
+ *  holds U*C*H*W floats; otherwise out is [U,C,H,W] and work may be NULL.
+ *  relu_out (nullable) receives relu(out) (matching_net.py:79).
+ *  out_absmax (nullable, device float[U], zeroed by the caller): raised to
+ *  max |out[u]| per unit (the split decoder's per-unit activation scale
+ *  source, TMR_SPLIT_XMAX_PER_UNIT), with no extra pass over out.
+ *  algo: TMR_XCORR_VALU (fp32 LDS-blocked wavefront kernels), TMR_XCORR_MFMA
+ *  (row-Toeplitz implicit GEMM on v_mfma_f32_16x16x32_{f16,bf16}: W % 32 == 0,
+ *  W <= 256, templates <= 31x31, tmpl_split given; TMR_E_UNSUPPORTED
+ *  otherwise) or TMR_XCORR_AUTO (MFMA when it fits, tmpl_split is given and
+ *  min_k -- the smallest template side of the launch -- reaches the
+ *  crossover; VALU otherwise).
+ *  tmpl_split / total_rows: tmr_template_split of the same templates and prec.
+ *  prec (TMR_PREC_*, below): the MFMA operands -- TMR_PREC_F16X3 the fp32
+ *  path's 3-term split (1e-5 contract); TMR_PREC_BF16 / TMR_PREC_F16 one
+ *  16-bit term with fp32 accumulation (config C's bf16 contract, 1e-2).  The
+ *  VALU kernels are fp32 whatever prec says.
+ *  out_bf16 = 1: out is bf16 [U][C][H][W], each element the round-to-nearest-
+ *  even bf16 of the fp32 value (the bf16 contract's detect path, whose decoder
+ *  records are those bf16 values); needs algo TMR_XCORR_MFMA, prec
+ *  TMR_PREC_BF16, squeeze 0 and relu_out NULL. */
 #define TMR_XCORR_AUTO 0
 #define TMR_XCORR_VALU 1
 #define TMR_XCORR_MFMA 2
-int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
-                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
-                   const float *scale, int squeeze, float *out, float *relu_out, float *work,
-                   float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
-                   int min_k, void *stream);
-/* Same with the MFMA kernel's operand precision chosen (prec, the TMR_PREC_*
- * codes below): TMR_PREC_F16X3 is tmr_xcorr_algo (the fp32 path's 1e-5
- * contract); TMR_PREC_BF16 / TMR_PREC_F16 run the MFMA kernel on ONE bf16 /
- * scaled-fp16 term per product with fp32 accumulation -- the bf16 MFMA path of
- * BASELINE config C (north_star "within a stated bf16 tolerance": <= 1e-2
- * normwise, tests/test_gpu_parity.py).  The VALU kernels are fp32 whatever
- * prec says.  tmpl_split must come from tmr_template_split_prec with the same
- * prec (TMR_PREC_F16 and TMR_PREC_F16X3 fragments are identical). */
-int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
-                   const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
-                   const float *scale, int squeeze, float *out, float *relu_out, float *work,
-                   float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
-                   int min_k, int prec, void *stream);
-/* tmr_xcorr_prec with the f_TM plane's element type chosen: out_bf16 = 0 is
- * tmr_xcorr_prec (out float [U][C][H][W]); out_bf16 = 1 writes out as bf16
- * [U][C][H][W], each element the round-to-nearest-even bf16 of the fp32
- * value tmr_xcorr_prec would write -- the bf16 contract's detect path, whose
- * decoder records (tmr_split_xpack16) are those bf16 values.  out_bf16 = 2 +
- * ks (ks 1/3/5/7, C % 32 == 0): `out` receives those decoder records
- * themselves (tmr_split_xpack16's layout for a ks x ks conv: the interior;
- * zero the ring with tmr_split_xpack_ring) -- no f_TM plane and no record
- * pass.  out_bf16 needs algo TMR_XCORR_MFMA, prec TMR_PREC_BF16, squeeze 0
- * and relu_out NULL (TMR_E_INVALID otherwise).  Same sources as
- * tmr_xcorr_prec: models/template_matching.py:23-41,97. */
-int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
-                  const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht, int max_wt,
-                  const float *scale, int squeeze, void *out, float *relu_out, float *work,
-                  float *out_absmax, const void *tmpl_split, int64_t total_rows, int algo,
-                  int min_k, int prec, int out_bf16, void *stream);
+typedef struct tmr_xcorr_args {
+    const float *f;
+    const float *templates;
+    const tmr_unit_t *units;
+    const int32_t *img_units;
+    const float *scale;
+    void *out;
+    float *relu_out;
+    float *work;
+    float *out_absmax;
+    const void *tmpl_split;
+    int64_t total_rows;
+    int32_t B, C, H, W;
+    int32_t U, max_ht, max_wt;
+    int32_t squeeze;
+    int32_t algo, min_k, prec, out_bf16;
+} tmr_xcorr_args_t;
+int tmr_xcorr(const tmr_xcorr_args_t *args, void *stream);
 /* Operand prep of the MFMA correlation: per (unit u, channel c) template
  * T = templates[units[u].tmpl_offset + c*ht*wt ...], t * 2^-e = th + tl with
  * fp16 hi/lo parts and 2^-e the power-of-two scale of max |T| (max |t| 2^-e <
@@ -161,29 +168,19 @@ int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templ
  * (C * row_offset(u) + c * ht * nk) * 2 + (i * nk + b) * 2 + k; then e
  * int32[U][C].  row_offset(u) = sum over earlier units of ht * nk(wt) and
  * total_rows = that sum over all units (tmr_unit_t.row_offset, set by the
- * host); size in bytes from tmr_template_split_size.  The exponents are
- * stored at row units[u].out_unit: a launch over a subset of a unit set
- * (absolute row_offset / out_unit) fills that set's buffer, sized with the
- * set's U and total_rows. */
-int64_t tmr_template_split_size(int U, int C, int64_t total_rows);
+ * host); size from tmr_size(TMR_SIZE_TEMPLATE_SPLIT, U, C, total_rows).
+ * prec: TMR_PREC_F16X3 writes hi and lo; the one-term precisions the hi
+ * fragments only (TMR_PREC_BF16: bf16; TMR_PREC_F16: the fp16 hi). */
 int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
-                       int64_t total_rows, void *out, void *stream);
-/* The same fragments in the operand format of tmr_xcorr_prec's prec:
- * TMR_PREC_F16X3 is tmr_template_split; the one-term precisions write the hi
- * fragments only (TMR_PREC_BF16: bf16 hi; TMR_PREC_F16: the fp16 hi of
- * tmr_template_split) and leave the lo slots unwritten (the one-term kernel
- * never reads them). */
-int tmr_template_split_prec(const float *templates, const tmr_unit_t *units, int U, int C,
-                            int64_t total_rows, int prec, void *out, void *stream);
+                       int64_t total_rows, int prec, void *out, void *stream);
 
 /* ---- (a10+a11+a12) conv stack: head partials ------------------------------
- * tmr_split_conv_heads (below) never stores the decoder activations: each
- * 128-channel tile t of the fused decoder_b || decoder_o GEMM writes
+ * tmr_split_conv with headw (below) never stores the decoder activations:
+ * each 128-channel tile t of the fused decoder_b || decoder_o GEMM writes
  *   partials[t][j][u][h][w] = sum_{n in tile t} act(conv)[n] * headw[n][j], j < 5
  * (headw [ceil(N/128)*128][5] fp32, zero padded; j 0-3 = ltrbs_head,
  * 4 = objectness_head, regression_head.py:31,50), and tmr_heads_reduce() sums
- * the tiles and adds the head biases.  Size in floats: */
-int64_t tmr_heads_partials_size(int N, int U, int H, int W);
+ * the tiles and adds the head biases.  Size: TMR_SIZE_HEADS_PARTIALS floats. */
 /* o [U,1,H,W] = head_bias[4] + sum_t partials[t][4];  b [U,4,H,W] (nullable) =
  * head_bias[j] + sum_t partials[t][j], t over ceil(N/tile_n) channel tiles
  * (tile_n = 128, the split kernel's tile; 64 is accepted too). */
@@ -203,17 +200,19 @@ int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int
  *                   normwise contract (config B);
  *   TMR_PREC_BF16:  one bf16 term, fp32 accumulation (config C, 1e-2 contract);
  *   TMR_PREC_F16:   one scaled fp16 term.
- * tmr_absmax: *out = max(|x|) (or max(*out, |x|) when accumulate), the scale
- * source for the packs and the conv (F16X3 / F16; NULL allowed for BF16).
- * tmr_absmax_rows: the same per sample, out[s] = max |x[s][0..n)| for
- * x [S][n].  tmr_scale_merge: out_img[b] = max(img_max[b] (nullable: 0),
+ * tmr_absmax_rows: out[s] = max |x[s][0..n)| for x [S][n] (or max(out[s], ...)
+ * when accumulate), the scale sources for the packs and the conv (F16X3 /
+ * F16; NULL allowed for BF16).  tmr_scale_merge: out_img[b] = max(img_max[b] (nullable: 0),
  * unit_max[u] over the units with unit_image[u] == b), out_unit[u] =
  * out_img[unit_image[u]] (out_img nullable) -- one scale per image for a
  * launch whose tiles read an image's src0 records and its units' src1
  * records together.
  * tmr_split_xpack: x [S][C][H][W] fp32 -> [S][ceil(C/32)*halves][Hp][Wp][64 B]
  * (halves 2 for F16X3: hi, lo), zero padded to whole 16x32 tiles plus the ks
- * halo (sizes in BYTES).  xmax_per_sample = 0: one scale source *xmax for
+ * halo (size TMR_SIZE_XPACK).  `up` bit TMR_XPACK_UPSAMPLE: the records are
+ * of up2x(x) (H, W are x's; the records' are 2H, 2W); bit TMR_XPACK_ONES: a
+ * constant-1 channel is appended (C + 1 channels; see tmr_split_fold_proj).
+ * xmax_per_sample = 0: one scale source *xmax for
  * every sample; 1: xmax[s] for sample s (float[S]); 2: xmax[s][y][x] per
  * (output-resolution) pixel, for TMR_SPLIT_XMAX_PER_PIXEL 1x1 convs.
  * Per-sample scales make a unit's arithmetic independent of the other units
@@ -229,39 +228,34 @@ int tmr_heads_reduce(const float *partials, int N, int tile_n, int U, int H, int
 #define TMR_PREC_F16X3 0
 #define TMR_PREC_BF16 1
 #define TMR_PREC_F16 2
-int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stream);
 int tmr_absmax_rows(const float *x, int S, int64_t n, int accumulate, float *out, void *stream);
 int tmr_scale_merge(const float *img_max, const float *unit_max, const int32_t *unit_image, int B, int U,
                     float *out_img, float *out_unit, void *stream);
-int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec);
-int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
+#define TMR_XPACK_UPSAMPLE 1
+#define TMR_XPACK_ONES 2
+int tmr_split_xpack(const float *x, int S, int C, int H, int W, int up, int ks, int prec,
                     const float *xmax, int xmax_per_sample, void *out, void *stream);
 /* tmr_split_xpack16: the TMR_PREC_BF16 records of a bf16 x [S][C][H][W]
- * (tmr_xcorr_out's bf16 f_TM; W % 8 == 0): bit-identical to tmr_split_xpack
+ * (tmr_xcorr's bf16 f_TM; W % 8 == 0): bit-identical to tmr_split_xpack
  * of the fp32 values those bf16 elements round. */
 int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
                       void *stream);
-/* tmr_split_xpack_ring: only the zero padding ring of the records of an
- * [S][C][H][W] input (the interior written elsewhere, e.g. by tmr_xcorr_out's
- * record mode). */
-int tmr_split_xpack_ring(void *out, int S, int C, int H, int W, int ks, int prec, void *stream);
-/* tmr_split_xpack_up: records of [up2x(f) (upsample) or f; 1 (ones)] from the
- * SAM features f [S][Cin][Hin][Win] (sizes: tmr_split_xpack_size with
- * C = Cin + ones at the output resolution).  With tmr_split_fold_proj it
- * feeds the decoder's fp half without materialising fp: conv(input_proj(x))
+/* tmr_split_fold_proj: with tmr_split_xpack's TMR_XPACK_UPSAMPLE | ONES
+ * records of the SAM features it feeds the decoder's fp half without
+ * materialising fp: conv(input_proj(x))
  * = conv'([x; 1]), W'[n][c] = sum_k Wd[n][k] P[k][c], W'[n][Cin] = sum_k
  * Wd[n][k] b[k] per tap (matching_net.py:27-30,56,63-69), fp64 accumulation;
  * out [N][Cin+1][ks][ks] from wd [N][Cw][ks][ks] (first Cp channels = fp). */
-int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample, int ones,
-                       int ks, int prec, const float *xmax, int xmax_per_sample, void *out, void *stream);
 int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
                         const float *proj_b, int Cin, float *out, void *stream);
-int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec);
 int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, const float *wmax,
                     void *out, void *stream);
-/* flags: TMR_SPLIT_TILED_OUT (store only): `out` receives the raw conv result
- * (no bias / activation) in the kernel's tiled accumulator layout,
- * tmr_split_acc_size(U, N, H, W) floats; TMR_SPLIT_TILED_INIT: `acc_init` is
+/* tmr_split_conv: headw NULL -- `out` [U][N][H][W] receives act(conv + bias);
+ * headw given -- `out` receives the head partials (above, TMR_SIZE_HEADS_PARTIALS
+ * floats) and the activations are never stored.
+ * flags: TMR_SPLIT_TILED_OUT (headw NULL only): `out` receives the raw conv
+ * result (no bias / activation) in the kernel's tiled accumulator layout,
+ * TMR_SIZE_ACC(U, N, H, W) floats; TMR_SPLIT_TILED_INIT: `acc_init` is
  * in that layout (indexed by unit_image), e.g. the per-image fp half. */
 #define TMR_SPLIT_TILED_OUT 1
 #define TMR_SPLIT_TILED_INIT 2
@@ -292,16 +286,10 @@ int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, int prec, con
 #define TMR_SPLIT_UNITS_PER_IMAGE_SHIFT 8
 /* out[s][p] = max_c |x[s][c][p]| for x [S][C][HW] */
 int tmr_pixel_absmax(const float *x, int S, int C, int64_t HW, float *out, void *stream);
-int64_t tmr_split_acc_size(int U, int N, int H, int W);
-int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
-                         int C1, int U, int H, int W, int ks, int prec, const void *wpack,
-                         const float *wmax, const float *xmax, const float *bias, int N,
-                         int leaky, const float *acc_init, float *out, int flags, void *stream);
-int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image, const void *xp1,
-                         int C1, int U, int H, int W, int ks, int prec, const void *wpack,
-                         const float *wmax, const float *xmax, const float *bias, int N,
-                         int leaky, const float *headw, const float *acc_init,
-                         float *partials, int flags, void *stream);
+int tmr_split_conv(const void *xp0, int C0, const int32_t *unit_image, const void *xp1, int C1, int U,
+                   int H, int W, int ks, int prec, const void *wpack, const float *wmax, const float *xmax,
+                   const float *bias, int N, int leaky, const float *headw, const float *acc_init,
+                   float *out, int flags, void *stream);
 
 /* ---- (a16) custom_shape_3x3_maxpool2d -----------------------------------
  * utils/TM_utils.py:337-361 on device fp32 planes x [planes][H][W]: out[e] =
@@ -347,10 +335,13 @@ int tmr_peaks_decode(const float *o, int input_is_prob, const float *reg, int U,
  * Outputs are written per image at cand_off[g]: keep-ordered logits [n,2] =
  * (score, 0), boxes [n,4], refs [n,2], optionally the keep indices (int64,
  * local to the image's union, = torchvision's return value) and kept[g].
- * Memory is O(total_cand) plus one bounded strip of IoU suppression words
- * (<= 256 MiB whatever n is): `work` holds
- * tmr_nms_work_size(total_cand, sum_nb, max_cand, G) bytes. */
-int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G);
+ * `work` holds TMR_SIZE_NMS_WORK(total_cand, sum_nb, max_cand, G) bytes:
+ * linear in the candidates, at most ~640 B per candidate (the suppressor
+ * lists take 512 B of it: 128 entries per row, sized per 64-row block), so
+ * the worst case -- every pixel of 16 units at 192^2 a candidate of one
+ * image, 589,824 rows -- needs ~0.38 GB.  An image of more than 655,360
+ * candidates is refused with TMR_E_INVALID (the greedy wave's LDS holds the
+ * kept bitmap), never truncated. */
 int tmr_nms(const float *logits, const float *box, const float *ref, const int32_t *counts,
             const int64_t *unit_off, const int32_t *seg_units, const int64_t *cand_off,
             const int64_t *nb_off,
@@ -379,8 +370,7 @@ int tmr_nms_small(const float *logits, const float *box, const float *ref, const
  * evaluation (numpy's float32 pairwise sums differ by a few fp32 ulps),
  * max = np.max(f) exactly, sparsity = np.mean(f <= 0) = count / n exactly.
  * Deterministic (fixed reduction order).  `work` holds
- * tmr_feature_stats_work_size(B) bytes. */
-int64_t tmr_feature_stats_work_size(int B);
+ * TMR_SIZE_STATS_WORK(B) bytes. */
 int tmr_feature_stats(const float *x, int B, int64_t n, void *work, double *out, void *stream);
 
 /* ---- the decode's reference-exp table, compact form ------------------------

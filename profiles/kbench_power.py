@@ -3,7 +3,7 @@
 The heads-launch variants (profiles/heads_variants.py) left
 the MFMA issue at a power-limited clock as the bound, and the variant that fed
 the MFMAs constant LDS contents ran 30% faster.  This times
-tmr_split_conv_store (3-term fp32 contract, 3x3, 512 -> 2048 channels at
+tmr_split_conv (3-term fp32 contract, 3x3, 512 -> 2048 channels at
 128^2, a batch of units) on the SAME launch with different activation data:
 standard normal, LayerNorm'd SAM-like features upsampled x2 (smooth), a real
 correlation output (f_TM), a constant, and zeros; weights reference-init or
@@ -72,8 +72,8 @@ def main():
             for _ in range(a.reps + 1):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, pc, ptr(wp), ptr(wmax),
-                     ptr(xmax), ptr(b), N, 1, None, ptr(out), 0, stream())
+                call("tmr_split_conv", ptr(xp), C, None, None, 0, U, H, W, ks, pc, ptr(wp), ptr(wmax),
+                     ptr(xmax), ptr(b), N, 1, None, None, ptr(out), 0, stream())
                 e.record()
                 torch.cuda.synchronize()
                 ms.append(s.elapsed_time(e))
@@ -112,8 +112,8 @@ def bits_sweep(a):
             for _ in range(a.reps + 1):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, pc, ptr(wp), ptr(wmax),
-                     ptr(xmax), ptr(b), N, 1, None, ptr(out), 0, stream())
+                call("tmr_split_conv", ptr(xp), C, None, None, 0, U, H, W, ks, pc, ptr(wp), ptr(wmax),
+                     ptr(xmax), ptr(b), N, 1, None, None, ptr(out), 0, stream())
                 e.record()
                 torch.cuda.synchronize()
                 ms.append(s.elapsed_time(e))

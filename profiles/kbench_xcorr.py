@@ -1,4 +1,4 @@
-"""Micro-benchmark of the correlation kernel (tmr_xcorr_algo) per template
+"""Micro-benchmark of the correlation kernel (tmr_xcorr) per template
 size and kernel: for each k, B images x E exemplars of k x k templates on
 fp [B,512,H,H]; HIP events around the xcorr launch on its stream (median of
 R repetitions).  One JSON line per (algo, k) with the SURVEY.md 8d roofline
@@ -83,8 +83,8 @@ def main():
         hout = torch.empty((a.heat_units, 2048, H, H), device=dev)
 
         def heat():
-            call("tmr_split_conv_store", ptr(hxp), 512, None, None, 0, a.heat_units, H, H, 3,
-                 PREC_CODES["fp32"], ptr(hwp), ptr(hwmax), ptr(hxmax), ptr(hb), 2048, 1, None, ptr(hout), 0,
+            call("tmr_split_conv", ptr(hxp), 512, None, None, 0, a.heat_units, H, H, 3,
+                 PREC_CODES["fp32"], ptr(hwp), ptr(hwmax), ptr(hxmax), ptr(hb), 2048, 1, None, None, ptr(hout), 0,
                  stream())
     for name, boxes, ks in sets:
         flops = float(sum(2.0 * C * (H - k + 1) ** 2 * k * k for k in ks))

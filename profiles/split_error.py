@@ -1,4 +1,4 @@
-"""Normwise error of the split decoder conv (tmr_split_conv_store, fp32
+"""Normwise error of the split decoder conv (tmr_split_conv, fp32
 contract) against an fp64 torch conv on decoder-shaped inputs: the weights'
 split scheme's precision (VARIANT selects the library, TMR_LIB_VARIANT)."""
 import json

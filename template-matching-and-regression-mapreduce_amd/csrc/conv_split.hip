@@ -843,27 +843,6 @@ __device__ __forceinline__ void absmax_commit(float m, unsigned *out) {
     if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
-__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ x, int64_t n, unsigned *__restrict__ out) {
-    float m = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        m = fmaxf(m, fabsf(x[i]));
-    absmax_commit(m, out);
-}
-
-__global__ __launch_bounds__(256) void absmax_vec_kernel(const float4 *__restrict__ x, int64_t n4,
-                                                         unsigned *__restrict__ out) {
-    float m = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 v = x[i];
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-    absmax_commit(m, out);
-}
-
-// per-sample max |x| (tmr_absmax_rows): row s = blockIdx.y, blocks along x
-// stride over it; one atomic per block (absmax_commit)
 __global__ __launch_bounds__(256) void absmax_rows_kernel(const float *__restrict__ x, int64_t n, int vec,
                                                           unsigned *__restrict__ out) {
     const float *xr = x + (size_t)blockIdx.y * n;
@@ -1246,25 +1225,6 @@ int xpack_launch(const float *x, int S, int Cin, int Hin, int Win, int ups, int 
 
 }  // namespace
 
-extern "C" int tmr_absmax(const float *x, int64_t n, int accumulate, float *out, void *stream) {
-    TMR_REQUIRE(out && n >= 0 && (n == 0 || x));
-    hipStream_t s = tmr_stream(stream);
-    if (!accumulate && hipMemsetAsync(out, 0, sizeof(float), s) != hipSuccess) return TMR_E_HIP;
-    if (n == 0) return TMR_OK;
-    unsigned *o = reinterpret_cast<unsigned *>(out);
-    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0) {
-        const int64_t n4 = n / 4;
-        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n4, 256 * 8), 512);
-        hipLaunchKernelGGL(absmax_vec_kernel, dim3(blocks), dim3(256), 0, s,
-                           reinterpret_cast<const float4 *>(x), n4, o);
-    } else {
-        const int blocks = (int)std::min<int64_t>(tmr_cdiv(n, 256 * 8), 512);
-        hipLaunchKernelGGL(absmax_kernel, dim3(blocks), dim3(256), 0, s, x, n, o);
-    }
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
-}
-
 extern "C" int tmr_absmax_rows(const float *x, int S, int64_t n, int accumulate, float *out, void *stream) {
     TMR_REQUIRE(out && S > 0 && S < 65536 && n >= 0 && (n == 0 || x));
     hipStream_t s = tmr_stream(stream);
@@ -1299,17 +1259,23 @@ extern "C" int tmr_scale_merge(const float *img_max, const float *unit_max, cons
     return TMR_OK;
 }
 
-extern "C" int64_t tmr_split_xpack_size(int S, int C, int H, int W, int ks, int prec) {
+int64_t tmr_xpack_bytes(int S, int C, int H, int W, int ks, int prec) {
     if (S <= 0 || C <= 0 || H <= 0 || W <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
     return (int64_t)S * tmr_cdiv(C, CCH) * prec_halves(prec) * pad_h(H, ks) * pad_w(W, ks) * XREC;
 }
 
-extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int ks, int prec,
+// up = 0: records of x itself (the 4-wide plain pack); TMR_XPACK_UPSAMPLE /
+// TMR_XPACK_ONES: of [up2x(x) or x; 1] straight from the SAM features
+extern "C" int tmr_split_xpack(const float *x, int S, int C, int H, int W, int up, int ks, int prec,
                                const float *xmax, int xmax_per_sample, void *out, void *stream) {
     TMR_REQUIRE(x && out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
+    TMR_REQUIRE((up & ~(TMR_XPACK_UPSAMPLE | TMR_XPACK_ONES)) == 0);
     TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
     TMR_REQUIRE(xmax_per_sample >= 0 && xmax_per_sample <= 2);
-    return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, xmax_per_sample, out, stream);
+    if (up == 0) return xpack_launch<0>(x, S, C, H, W, 0, 0, H, W, ks, prec, xmax, xmax_per_sample, out, stream);
+    const int ups = (up & TMR_XPACK_UPSAMPLE) ? 1 : 0, ones = (up & TMR_XPACK_ONES) ? 1 : 0;
+    return xpack_launch<1>(x, S, C, H, W, ups, ones, ups ? 2 * H : H, ups ? 2 * W : W, ks, prec, xmax,
+                           xmax_per_sample, out, stream);
 }
 
 extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int ks, int prec, void *out,
@@ -1328,43 +1294,6 @@ extern "C" int tmr_split_xpack16(const void *x, int S, int C, int H, int W, int 
     return TMR_OK;
 }
 
-extern "C" int tmr_split_xpack_ring(void *out, int S, int C, int H, int W, int ks, int prec, void *stream) {
-    TMR_REQUIRE(out && S > 0 && C > 0 && H > 0 && W > 0 && ks_ok(ks) && prec_ok(prec));
-    const int NCc = (int)tmr_cdiv(C, CCH), Hp = pad_h(H, ks), Wp = pad_w(W, ks);
-    const int64_t nbord = (int64_t)Hp * Wp - (int64_t)H * W;
-    const dim3 g((unsigned)tmr_cdiv(nbord * S * NCc, 256));
-    if (nbord == 0) return TMR_OK;
-    hipStream_t s = tmr_stream(stream);
-    // xpack4_kernel with no row segments: every block writes the zero ring
-    switch (prec) {
-        case TMR_PREC_F16X3:
-            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_F16X3>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
-                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<h8 *>(out));
-            break;
-        case TMR_PREC_BF16:
-            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_BF16>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
-                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<b8 *>(out));
-            break;
-        default:
-            hipLaunchKernelGGL((xpack4_kernel<TMR_PREC_F16>), g, dim3(256), 0, s, (const float *)nullptr, S, C, H, W, NCc, Hp, Wp,
-                               ks / 2, (int64_t)0, nbord, (const float *)nullptr, 0, static_cast<h8 *>(out));
-            break;
-    }
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
-}
-
-extern "C" int tmr_split_xpack_up(const float *f, int S, int Cin, int Hin, int Win, int upsample,
-                                  int ones, int ks, int prec, const float *xmax, int xmax_per_sample,
-                                  void *out, void *stream) {
-    TMR_REQUIRE(f && out && S > 0 && Cin > 0 && Hin > 0 && Win > 0 && ks_ok(ks) && prec_ok(prec));
-    TMR_REQUIRE(prec == TMR_PREC_BF16 || xmax);
-    TMR_REQUIRE(xmax_per_sample >= 0 && xmax_per_sample <= 2);
-    const int H = upsample ? 2 * Hin : Hin, W = upsample ? 2 * Win : Win;
-    return xpack_launch<1>(f, S, Cin, Hin, Win, upsample ? 1 : 0, ones ? 1 : 0, H, W, ks, prec, xmax,
-                           xmax_per_sample, out, stream);
-}
-
 extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int ks, const float *proj_w,
                                    const float *proj_b, int Cin, float *out, void *stream) {
     TMR_REQUIRE(wd && proj_w && proj_b && out && N > 0 && Cp > 0 && Cw >= Cp && Cin > 0 && ks > 0);
@@ -1375,12 +1304,12 @@ extern "C" int tmr_split_fold_proj(const float *wd, int N, int Cw, int Cp, int k
     return TMR_OK;
 }
 
-extern "C" int64_t tmr_split_acc_size(int U, int N, int H, int W) {
+int64_t tmr_acc_floats(int U, int N, int H, int W) {
     if (U <= 0 || N <= 0 || H <= 0 || W <= 0) return -1;
     return (int64_t)U * tmr_cdiv(N, BM) * BM * tmr_cdiv(H, TH) * TH * tmr_cdiv(W, TW) * TW;
 }
 
-extern "C" int64_t tmr_split_wpack_size(int N, int C0, int C1, int ks, int prec) {
+int64_t tmr_wpack_bytes(int N, int C0, int C1, int ks, int prec) {
     if (N <= 0 || C0 < 0 || C1 < 0 || C0 + C1 <= 0 || !ks_ok(ks) || !prec_ok(prec)) return -1;
     return (int64_t)ks * ks * (tmr_cdiv(C0, CCH) + tmr_cdiv(C1, CCH)) * tmr_cdiv(N, BM) * BM *
            prec_wrec(prec);
@@ -1413,23 +1342,15 @@ extern "C" int tmr_split_wpack(const float *w, int N, int C0, int C1, int ks, in
     return TMR_OK;
 }
 
-extern "C" int tmr_split_conv_store(const void *xp0, int C0, const int32_t *unit_image,
-                                    const void *xp1, int C1, int U, int H, int W, int ks, int prec,
-                                    const void *wpack, const float *wmax, const float *xmax,
-                                    const float *bias, int N, int leaky, const float *acc_init,
-                                    float *out, int flags, void *stream) {
+extern "C" int tmr_split_conv(const void *xp0, int C0, const int32_t *unit_image, const void *xp1, int C1, int U,
+                              int H, int W, int ks, int prec, const void *wpack, const float *wmax, const float *xmax,
+                              const float *bias, int N, int leaky, const float *headw, const float *acc_init,
+                              float *out, int flags, void *stream) {
     TMR_REQUIRE(out);
-    return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
-                        leaky, acc_init, out, nullptr, nullptr, 0, flags, stream);
-}
-
-extern "C" int tmr_split_conv_heads(const void *xp0, int C0, const int32_t *unit_image,
-                                    const void *xp1, int C1, int U, int H, int W, int ks, int prec,
-                                    const void *wpack, const float *wmax, const float *xmax,
-                                    const float *bias, int N, int leaky, const float *headw,
-                                    const float *acc_init, float *partials, int flags,
-                                    void *stream) {
-    TMR_REQUIRE(headw && partials && !(flags & TMR_SPLIT_TILED_OUT));
-    return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N,
-                        leaky, acc_init, nullptr, headw, partials, 1, flags, stream);
+    if (!headw)  // activations (or the raw tiled accumulator) to out
+        return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N, leaky,
+                            acc_init, out, nullptr, nullptr, 0, flags, stream);
+    TMR_REQUIRE(!(flags & TMR_SPLIT_TILED_OUT));  // the head partials of the fused epilogue to out
+    return split_common(xp0, C0, unit_image, xp1, C1, U, H, W, ks, prec, wpack, wmax, xmax, bias, N, leaky, acc_init,
+                        nullptr, headw, out, 1, flags, stream);
 }

@@ -784,7 +784,7 @@ __global__ __launch_bounds__(SMALL_N) void nms_small_dev_kernel(
 
 }  // namespace
 
-extern "C" int64_t tmr_nms_work_size(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
+int64_t tmr_nms_work_bytes(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G) {
     if (total_cand < 0 || sum_nb < 0 || max_cand < 0 || G <= 0) return -1;
     return work_bytes(total_cand, sum_nb, G);
 }

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64) void stats_final_kernel(const float *__restrict
 
 }  // namespace
 
-extern "C" int64_t tmr_feature_stats_work_size(int B) {
+int64_t tmr_stats_work_bytes(int B) {
     if (B < 0) return -1;
     return (int64_t)B * SLICES * 4 * (int64_t)sizeof(double);
 }

@@ -10,6 +10,17 @@
 
 #include "../../include/tmr.h"
 
+// Library-internal functions shared between the sources (not part of the
+// ABI: hidden, the one sizing entry point tmr_size dispatches to them).
+#define TMR_INTERNAL __attribute__((visibility("hidden")))
+TMR_INTERNAL int64_t tmr_template_split_bytes(int U, int C, int64_t total_rows);
+TMR_INTERNAL int64_t tmr_heads_partials_floats(int N, int U, int H, int W);
+TMR_INTERNAL int64_t tmr_xpack_bytes(int S, int C, int H, int W, int ks, int prec);
+TMR_INTERNAL int64_t tmr_wpack_bytes(int N, int C0, int C1, int ks, int prec);
+TMR_INTERNAL int64_t tmr_acc_floats(int U, int N, int H, int W);
+TMR_INTERNAL int64_t tmr_nms_work_bytes(int64_t total_cand, int64_t sum_nb, int64_t max_cand, int G);
+TMR_INTERNAL int64_t tmr_stats_work_bytes(int B);
+
 #define TMR_CHECK_LAUNCH()                                  \
     do {                                                    \
         hipError_t e_ = hipGetLastError();                  \

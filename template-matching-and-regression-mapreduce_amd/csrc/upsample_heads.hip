@@ -106,7 +106,7 @@ extern "C" int tmr_upsample2x(const float *feat, int BC, int Hin, int Win, float
     return launch_upsample2x(feat, BC, Hin, Win, out, tmr_stream(stream));
 }
 
-extern "C" int64_t tmr_heads_partials_size(int N, int U, int H, int W) {
+int64_t tmr_heads_partials_floats(int N, int U, int H, int W) {
     if (N <= 0 || U <= 0 || H <= 0 || W <= 0) return -1;
     return tmr_cdiv(N, 64) * NHEAD * (int64_t)U * H * W;  // enough for 64- and 128-wide tiles
 }

@@ -71,7 +71,7 @@ __device__ __forceinline__ void unit_max_flush(const unsigned *slots, const tmr_
     __syncthreads();
     for (int i = threadIdx.x; i < min(nu, UMAX); i += blockDim.x) {
         const unsigned m = slots[i];
-        if (m) atomicMax(gout + units[u_beg + i].out_unit, m);
+        if (m) atomicMax(gout + u_beg + i, m);
     }
 }
 
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(NT) void xcorr_kernel(XArgs a, const float *__restr
         float vmax = 0.0f;
         const tmr_unit_t &un = a.units[u];
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane
+        const int uo = u;  // output plane
         const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
         float vmax = 0.0f;
         const tmr_unit_t &un = units[u];  // restrict: scalar loads, no wait behind the stores
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane
+        const int uo = u;  // output plane
         const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
         const int ph = h / 2, pw = w / 2;
@@ -565,10 +565,6 @@ struct MArgs {
     int SB;     // LDS plane row stride in bytes (32 mod 64)
     int LR;     // staged rows: band rows + 2 * HG
     int HG;     // max template height / 2
-    int HTM;    // max template height (template LDS rows per term)
-    int WTM;    // max template width
-    int rks;    // OB records mode: the decoder's kernel size (0: a bf16 [U][C][H][W] plane)
-    int rHp, rWp, rNC;  // records geometry (tmr_split_xpack16): padded rows, cols, 32-channel chunks
     int nband;  // bands per channel plane
     int nlog;   // logical blocks = nband * C * B
 };
@@ -679,7 +675,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 if (lo_too) *reinterpret_cast<h8 *>(f + AFRAG) = lo;  // the 3-term kernel's tl
             }
         }
-    if (lane == 0) exps[(int64_t)un.out_unit * C + c] = et;  // (the unit's row in the full set)
+    if (lane == 0) exps[(int64_t)u * C + c] = et;
 }
 
 // one unit over the band: acc[t] += sum_i A_i B_i over the wave's NTW tiles
@@ -745,52 +741,10 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
     }
 }
 
-// The same accumulation with the A fragments built in registers from the
-// unit's fp32 template staged in LDS (tsm [h][w], scaled by st = 2^-et):
-// lane (m, g) of row i, K block nk holds T[i][8g + 32nk + q - m - s] * st as
-// hi (and lo) 16-bit parts -- bit for bit tmr_template_split's fragments, with
-// no fragment pass over HBM and no L2 round trip per template row (the A
-// loads' latency was 17% of the config-B launch).
-template <int NTW, int NK, int WPR, int PM>
-__device__ __forceinline__ void mfma_unit_lds(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
-                                              int h, int w, const float *tsm, float st, int s, int tcol0,
-                                              int pw_al, int g, int m) {
-    typedef typename XOp<PM>::V8 V;
-    typedef typename XOp<PM>::E E;
-    constexpr bool SPLIT = XOp<PM>::SPLIT;
-    for (int i = 0; i < h; ++i) {
-        const char *rh = Fh + (size_t)(rb + i) * SB, *rl = Fl + (size_t)(rb + i) * SB;
-        const float *tr = tsm + i * w;
-#pragma unroll
-        for (int nk = 0; nk < NK; ++nk) {
-            V ch, cl;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int j = 8 * g + 32 * nk + q - m - s;
-                const float x = (j >= 0 && j < w) ? tr[j] * st : 0.0f;
-                const E hq = (E)x;
-                ch[q] = hq;
-                if (SPLIT) cl[q] = (E)(x - (float)hq);
-            }
-#pragma unroll
-            for (int t = 0; t < NTW; ++t) {
-                const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-                const V bh = *reinterpret_cast<const V *>(rh + colb);
-                acc[t] = xmma(ch, bh, acc[t]);
-                if (SPLIT) {
-                    const V bl = *reinterpret_cast<const V *>(rl + colb);
-                    acc[t] = xmma(ch, bl, acc[t]);
-                    acc[t] = xmma(cl, bh, acc[t]);
-                }
-            }
-        }
-    }
-}
-
 // OB: f_TM leaves as bf16 (the bf16 contract's detect path: the decoder's
 // bf16 records are bf16(f_TM) either way, so the fp32 plane is never needed;
 // half the bytes written here and read by the record pack)
-template <int NTW, int NV4, int TRB, int PM, bool OB = false, bool TL = false, bool RC = false>
+template <int NTW, int NV4, int TRB, int PM, bool OB = false>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
@@ -815,11 +769,6 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     char *Fh = smem, *Fl = smem + (size_t)LR * SB;  // Fl: F16X3 only
     float *red = reinterpret_cast<float *>(smem + NPL * (size_t)LR * SB);
     unsigned *slots = reinterpret_cast<unsigned *>(red + 16);  // [UMAX] per-unit max |out|
-    float *tsm = reinterpret_cast<float *>(slots + UMAX);       // [HTM][WTM] template (trows == NULL)
-    // TL: A fragments built in-kernel from the LDS template (a separate
-    // instantiation: both paths in one kernel cost registers and occupancy,
-    // measured +14% at config B, profiles/r05d)
-    constexpr bool tl = TL;
     const int tid = threadIdx.x;
     const bool umax = a.out_absmax && !a.squeeze;
     if (tid < UMAX) slots[tid] = 0u;  // (ordered before the uses by block_max's barriers)
@@ -888,24 +837,9 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         float vmax = 0.0f;
         const tmr_unit_t &un = units[u];
         const int h = __builtin_amdgcn_readfirstlane(un.ht), w = __builtin_amdgcn_readfirstlane(un.wt);
-        const int uo = __builtin_amdgcn_readfirstlane(un.out_unit);  // output plane (texp row)
+        const int uo = u;  // output plane (texp row)
         const int roff = __builtin_amdgcn_readfirstlane(un.row_offset);
-        int et = 0;
-        float st = 1.0f;
-        if (tl) {  // stage the (unit, channel) template; its power-of-two scale per wave
-            const int64_t toff = ((int64_t)__builtin_amdgcn_readfirstlane((int)(un.tmpl_offset >> 32)) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)un.tmpl_offset);
-            const float *tg = a.tmpl + toff + (int64_t)c * h * w;
-            __syncthreads();  // every wave is done with the previous unit's template
-            for (int e = tid; e < h * w; e += NT) tsm[e] = tg[e];
-            __syncthreads();
-            float mt = 0.0f;
-            for (int e = tid & 63; e < h * w; e += 64) mt = fmaxf(mt, fabsf(tsm[e]));
-            for (int o = 32; o > 0; o >>= 1) mt = fmaxf(mt, __shfl_xor(mt, o));
-            st = pow2_scale(mt, et);
-        } else {
-            et = __builtin_amdgcn_readfirstlane(texp[(size_t)uo * a.C + c]);
-        }
+        const int et = __builtin_amdgcn_readfirstlane(texp[(size_t)uo * a.C + c]);
         const int ph = h / 2, pw = w / 2, Ho = H - h + 1, Wo = W - w + 1;
         const int pw_al = (pw + 7) & ~7, s = pw_al - pw;
         f32x4 acc[NTW];
@@ -913,19 +847,12 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         if (row_live) {
             const int rb = tr * 16 + l16 + hg - ph;  // LDS row of output row (yb0 + 16 tr + l16) at i = 0
-            if (tl) {
-                if (16 + s + w - 1 <= 32)
-                    mfma_unit_lds<NTW, 1, WPR, PM>(acc, Fh, Fl, SB, rb, h, w, tsm, st, s, tcol0, pw_al, g, l16);
-                else
-                    mfma_unit_lds<NTW, 2, WPR, PM>(acc, Fh, Fl, SB, rb, h, w, tsm, st, s, tcol0, pw_al, g, l16);
-            } else {
-                const char *arow = reinterpret_cast<const char *>(trows) +
-                                   ((int64_t)a.C * roff + (int64_t)c * h * tsplit_nk(w)) * 2 * AFRAG + lane * 16;
-                if (16 + s + w - 1 <= 32)
-                    mfma_unit<NTW, 1, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
-                else
-                    mfma_unit<NTW, 2, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
-            }
+            const char *arow = reinterpret_cast<const char *>(trows) +
+                               ((int64_t)a.C * roff + (int64_t)c * h * tsplit_nk(w)) * 2 * AFRAG + lane * 16;
+            if (16 + s + w - 1 <= 32)
+                mfma_unit<NTW, 1, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+            else
+                mfma_unit<NTW, 2, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
         }
         // ---- epilogue: exact unscale, correctly rounded /(h*w), scale, pad mask
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
@@ -947,19 +874,6 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                     const int xx = x + j;
                     r4[j] = (vy && xx >= pw && xx < pw + Wo) ? div_cr(acc[t][j] * inv, denom, rden) * sc : 0.0f;
                     vmax = fmaxf(vmax, fabsf(r4[j]));
-                }
-                if (RC) {
-                    // the decoder's bf16 records directly (tmr_split_xpack16's layout: piece
-                    // (c / 8) % 4 of chunk c / 32, element c % 8 of each pixel's 16 B): no
-                    // f_TM plane, no record pass; the 8 channels of a piece come from 8
-                    // consecutive blocks of this XCD, so their 2-B stores meet in its L2
-                    const int pad = m.rks / 2;
-                    __bf16 *rb = reinterpret_cast<__bf16 *>(outp) +
-                                 ((((size_t)uo * m.rNC + (c >> 5)) * 4 + ((c >> 3) & 3)) * m.rHp + y + pad) * m.rWp * 8 +
-                                 (size_t)(x + pad) * 8 + (c & 7);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) rb[8 * j] = (__bf16)r4[j];
-                    continue;
                 }
                 if (OB) {
                     *reinterpret_cast<b4 *>(reinterpret_cast<__bf16 *>(op) + (size_t)y * W + x) =
@@ -1042,28 +956,10 @@ static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
 template <int NTW, int NV4, int TRB, int PM, bool OB>
 static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp) {
-    constexpr bool can_tl = PM == TMR_PREC_F16X3 && !OB;  // in-kernel fragments: 3-term only
-    const bool tl = trows == nullptr;
-    if (tl && !can_tl) return TMR_E_UNSUPPORTED;
-    // record output (OB only) and in-kernel fragments: instantiations of
-    // their own -- a runtime branch in the epilogue cost the plain bf16 plane
-    // launch 3.0 -> 3.7 ms at config C (registers), profiles/r05g
-    const bool rc = OB && m.rks != 0;
-    const void *kfn = tl   ? (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, can_tl>
-                      : rc ? (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false, OB>
-                           : (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false>;
-    if (lds > 64 * 1024 &&
-        tmr_set_max_lds(kfn, lds) != hipSuccess)
-        return TMR_E_HIP;
-    if (tl)
-        hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, can_tl>), dim3(nblk), dim3(NT), lds, s, a, m,
-                           trows, texp, a.out, a.units);
-    else if (rc)
-        hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false, OB>), dim3(nblk), dim3(NT), lds, s, a,
-                           m, trows, texp, a.out, a.units);
-    else
-        hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB, false>), dim3(nblk), dim3(NT), lds, s, a, m,
-                           trows, texp, a.out, a.units);
+    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>;
+    if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows, texp,
+                       a.out, a.units);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
@@ -1077,25 +973,44 @@ static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
     case K:                                                                                    \
         return nv4 == 8 ? launch_mfma_t<K, 8, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp)    \
                         : launch_mfma_t<K, 16, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp);
-        TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8)
+        TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8) TMR_NTW(12)
 #undef TMR_NTW
         default: return TMR_E_UNSUPPORTED;
     }
 }
 
-static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, int max_wt,
-                       const void *tmpl_split, int64_t total_rows, int prec, bool out16, int rks) {
+template <int TRB>
+static int launch_mfma_p(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
+                         const _Float16 *trows, const int32_t *texp, int nv4, int prec, bool out16) {
+    if (out16)
+        return prec == TMR_PREC_BF16 ? launch_mfma_w<TRB, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp, nv4)
+                                     : TMR_E_UNSUPPORTED;
+    switch (prec) {
+        case TMR_PREC_F16X3: return launch_mfma_w<TRB, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_BF16: return launch_mfma_w<TRB, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_F16: return launch_mfma_w<TRB, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp, nv4);
+        default: return TMR_E_INVALID;
+    }
+}
+
+// Band height: 64 output rows (4 tile rows, one per wave, every tile column
+// of the row per wave) when the band and its halo fit the staging registers
+// and the row is 8 or 12 tiles wide; else 32 rows (2 tile rows, 2 waves per
+// row).  Measured (round 6, kbench_xcorr, one box, two reps): config-B mix
+// 4.77 / 4.75 -> 4.42 / 4.45 ms (fp32, 3 terms), config-C mix 3.22 / 3.20 ->
+// 2.80 / 2.77 ms (one bf16 term): half the bands, so half the A-fragment
+// fetches and halo re-stages per output, 8-12 independent accumulators per
+// wave and three template rows of A prefetch.
+static int band_tiles(int W, int max_ht) {
+    const int64_t lr4 = 64 + 2 * (max_ht / 2);
+    return (lr4 * W <= (int64_t)MAXV4 * NT * 4 && (W / 16 == 8 || W / 16 == 12)) ? 4 : 2;
+}
+
+static int launch_mfma(const XArgs &a, hipStream_t s, int B, int max_ht, int max_wt, const void *tmpl_split,
+                       int64_t total_rows, int prec, bool out16) {
     MArgs m;
-    m.rks = rks;
-    m.rHp = (int)tmr_cdiv(a.H, 16) * 16 + rks - 1;  // conv_split.hip pad_h / pad_w
-    m.rWp = (int)tmr_cdiv(a.W, 32) * 32 + rks - 1;
-    m.rNC = (int)tmr_cdiv(a.C, 32);
-    // 32-row bands (16-row bands, 2 more blocks per CU at k = 31: measured
-    // 1.7-1.9x slower at k >= 17, profiles/archive/r02b_kbench_xcorr_*)
-    const int trb = 2;
+    const int trb = band_tiles(a.W, max_ht);
     m.HG = max_ht / 2;
-    m.HTM = max_ht;
-    m.WTM = max_wt;
     m.LR = 16 * trb + 2 * m.HG;
     const int nk_max = (16 + 7 + max_wt - 1 + 31) / 32;
     m.SB = mfma_row_stride(2 * (a.W + MPADL + 32 * nk_max));
@@ -1103,34 +1018,23 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int U, int max_ht, 
     const int64_t nlog = (int64_t)m.nband * a.C * B;
     TMR_REQUIRE(nlog < (1LL << 31) - 8);
     m.nlog = (int)nlog;
-    const size_t lds = (prec == TMR_PREC_F16X3 ? 2 : 1) * (size_t)m.LR * m.SB + 64 + 4 * UMAX +
-                       (tmpl_split ? 0 : 4 * (size_t)max_ht * max_wt);
+    const size_t lds = (prec == TMR_PREC_F16X3 ? 2 : 1) * (size_t)m.LR * m.SB + 64 + 4 * UMAX;
     const unsigned nblk = (unsigned)((nlog + 7) / 8 * 8);
-    // tmpl_split NULL: the kernel builds the A fragments itself (mfma_unit_lds)
     const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
-    const int32_t *texp = tmpl_split ? reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
-                                                                         (int64_t)a.C * total_rows * 2 * AFRAG)
-                                     : nullptr;
-    (void)U;
+    const int32_t *texp = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
+                                                            (int64_t)a.C * total_rows * 2 * AFRAG);
     const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
-    if (out16)
-        return prec == TMR_PREC_BF16 ? launch_mfma_w<2, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp, nv4)
-                                     : TMR_E_UNSUPPORTED;
-    switch (prec) {
-        case TMR_PREC_F16X3: return launch_mfma_w<2, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
-        case TMR_PREC_BF16: return launch_mfma_w<2, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
-        case TMR_PREC_F16: return launch_mfma_w<2, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp, nv4);
-        default: return TMR_E_INVALID;
-    }
+    return trb == 4 ? launch_mfma_p<4>(a, m, lds, nblk, s, trows, texp, nv4, prec, out16)
+                    : launch_mfma_p<2>(a, m, lds, nblk, s, trows, texp, nv4, prec, out16);
 }
 
-extern "C" int64_t tmr_template_split_size(int U, int C, int64_t total_rows) {
+int64_t tmr_template_split_bytes(int U, int C, int64_t total_rows) {
     if (U <= 0 || C <= 0 || total_rows <= 0) return -1;
     return (int64_t)C * total_rows * 2 * AFRAG + 4 * (int64_t)U * C;
 }
 
-extern "C" int tmr_template_split_prec(const float *templates, const tmr_unit_t *units, int U, int C,
-                                       int64_t total_rows, int prec, void *out, void *stream) {
+extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
+                                  int64_t total_rows, int prec, void *out, void *stream) {
     TMR_REQUIRE(templates && units && out && U > 0 && C > 0 && total_rows > 0);
     TMR_REQUIRE(prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16);
     char *frags = reinterpret_cast<char *>(out);
@@ -1143,50 +1047,44 @@ extern "C" int tmr_template_split_prec(const float *templates, const tmr_unit_t 
     return TMR_OK;
 }
 
-extern "C" int tmr_template_split(const float *templates, const tmr_unit_t *units, int U, int C,
-                                  int64_t total_rows, void *out, void *stream) {
-    return tmr_template_split_prec(templates, units, U, C, total_rows, TMR_PREC_F16X3, out, stream);
-}
-
-extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const float *templates,
-                             const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                             int max_wt, const float *scale, int squeeze, void *out, float *relu_out,
-                             float *work, float *out_absmax, const void *tmpl_split,
-                             int64_t total_rows, int algo, int min_k, int prec, int out_bf16,
-                             void *stream) {
-    TMR_REQUIRE(f && templates && units && img_units && scale && out && B > 0 && C > 0 && U > 0);
+extern "C" int tmr_xcorr(const tmr_xcorr_args_t *x, void *stream) {
+    TMR_REQUIRE(x);
+    const int B = x->B, C = x->C, H = x->H, W = x->W, U = x->U, max_ht = x->max_ht, max_wt = x->max_wt;
+    TMR_REQUIRE(x->f && x->templates && x->units && x->img_units && x->scale && x->out && B > 0 && C > 0 &&
+                U > 0 && H > 0 && W > 0);
+    TMR_REQUIRE(x->out_bf16 == 0 || x->out_bf16 == 1);
     // a bf16 f_TM plane: the one-term bf16 MFMA kernel only, no relu / squeeze outputs
-    TMR_REQUIRE(!out_bf16 || (algo == TMR_XCORR_MFMA && prec == TMR_PREC_BF16 && !squeeze && !relu_out));
-    // out_bf16 = 2 + ks: the bf16 decoder records of a ks x ks decoder conv
-    const int rks = out_bf16 >= 2 ? out_bf16 - 2 : 0;
-    TMR_REQUIRE(out_bf16 < 2 || ((rks == 1 || rks == 3 || rks == 5 || rks == 7) && C % 32 == 0));
+    TMR_REQUIRE(!x->out_bf16 ||
+                (x->algo == TMR_XCORR_MFMA && x->prec == TMR_PREC_BF16 && !x->squeeze && !x->relu_out));
     TMR_REQUIRE(max_ht >= 1 && max_wt >= 1 && max_ht <= H && max_wt <= W);
-    TMR_REQUIRE(!squeeze || work);
-    TMR_REQUIRE(algo >= TMR_XCORR_AUTO && algo <= TMR_XCORR_MFMA);
-    TMR_REQUIRE(prec == TMR_PREC_F16X3 || prec == TMR_PREC_BF16 || prec == TMR_PREC_F16);
+    TMR_REQUIRE(!x->squeeze || x->work);
+    TMR_REQUIRE(x->algo >= TMR_XCORR_AUTO && x->algo <= TMR_XCORR_MFMA);
+    TMR_REQUIRE(x->prec == TMR_PREC_F16X3 || x->prec == TMR_PREC_BF16 || x->prec == TMR_PREC_F16);
+    TMR_REQUIRE(C < 65536 && B < 65536);
     XArgs a;
-    a.f = f;
-    a.tmpl = templates;
-    a.units = units;
-    a.img_units = img_units;
-    a.scale = scale;
-    a.out = static_cast<float *>(out);  // bf16 elements when out_bf16
-    a.relu_out = relu_out;
-    a.work = work;
-    a.out_absmax = reinterpret_cast<unsigned *>(out_absmax);
+    a.f = x->f;
+    a.tmpl = x->templates;
+    a.units = x->units;
+    a.img_units = x->img_units;
+    a.scale = x->scale;
+    a.out = static_cast<float *>(x->out);  // bf16 elements when out_bf16
+    a.relu_out = x->relu_out;
+    a.work = x->work;
+    a.out_absmax = reinterpret_cast<unsigned *>(x->out_absmax);
     a.C = C;
     a.H = H;
     a.W = W;
-    a.squeeze = squeeze;
+    a.squeeze = x->squeeze;
     hipStream_t s = tmr_stream(stream);
-    TMR_REQUIRE(C < 65536 && B < 65536);
-    const bool fits = mfma_fits(H, W, max_ht, max_wt) && (!tmpl_split || total_rows > 0);
-    if (algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
-    const bool use_mfma = algo == TMR_XCORR_MFMA || (algo == TMR_XCORR_AUTO && fits && min_k >= kMfmaMinK);
+    // the MFMA kernel reads its A fragments from tmpl_split (tmr_template_split)
+    const bool fits = mfma_fits(H, W, max_ht, max_wt) && x->tmpl_split && x->total_rows > 0;
+    if (x->algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
+    const bool use_mfma = x->algo == TMR_XCORR_MFMA || (x->algo == TMR_XCORR_AUTO && fits && x->min_k >= kMfmaMinK);
     if (use_mfma) {
-        const int rc = launch_mfma(a, s, B, U, max_ht, max_wt, tmpl_split, total_rows, prec, out_bf16 != 0, rks);
+        const int rc = launch_mfma(a, s, B, max_ht, max_wt, x->tmpl_split, x->total_rows, x->prec, x->out_bf16 != 0);
         if (rc != TMR_OK) return rc;
     } else {
+        TMR_REQUIRE(!x->out_bf16);
         // row-tiled kernel when rows are 16-B aligned and templates fit its
         // width specialisations (template sizes are odd, template_matching.py:66-73)
         const bool rows = (W % 4) == 0 && max_wt <= 31;
@@ -1203,9 +1101,7 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
         const bool narrow = max_wt <= 15;
         const void *kfn = !rows ? (const void *)xcorr_kernel
                           : narrow ? (const void *)xcorr_rows_kernel<15> : (const void *)xcorr_rows_kernel<31>;
-        if (lds > 64 * 1024 &&
-            tmr_set_max_lds(kfn, lds) != hipSuccess)
-            return TMR_E_HIP;
+        if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
         dim3 grid((unsigned)tmr_cdiv(H, RB), (unsigned)C, (unsigned)B);
         if (rows && narrow)
             hipLaunchKernelGGL(xcorr_rows_kernel<15>, grid, dim3(NT), lds, s, a, a.tmpl, a.out, a.units);
@@ -1215,39 +1111,12 @@ extern "C" int tmr_xcorr_out(const float *f, int B, int C, int H, int W, const f
             hipLaunchKernelGGL(xcorr_kernel, grid, dim3(NT), lds, s, a, a.tmpl, a.out);
         TMR_CHECK_LAUNCH();
     }
-    if (squeeze) {
+    if (x->squeeze) {
         int64_t tot = (int64_t)U * H * W;
-        hipLaunchKernelGGL(xcorr_squeeze_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, s,
-                           work, units, U, C, H, W, scale, a.out, relu_out,
-                           reinterpret_cast<unsigned *>(out_absmax));
+        hipLaunchKernelGGL(xcorr_squeeze_kernel, dim3((unsigned)tmr_cdiv(tot, 256)), dim3(256), 0, s, x->work,
+                           x->units, U, C, H, W, x->scale, a.out, x->relu_out,
+                           reinterpret_cast<unsigned *>(x->out_absmax));
         TMR_CHECK_LAUNCH();
     }
     return TMR_OK;
-}
-
-extern "C" int tmr_xcorr_prec(const float *f, int B, int C, int H, int W, const float *templates,
-                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                              float *work, float *out_absmax, const void *tmpl_split,
-                              int64_t total_rows, int algo, int min_k, int prec, void *stream) {
-    return tmr_xcorr_out(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
-                         relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, prec, 0, stream);
-}
-
-extern "C" int tmr_xcorr_algo(const float *f, int B, int C, int H, int W, const float *templates,
-                              const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                              int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                              float *work, float *out_absmax, const void *tmpl_split,
-                              int64_t total_rows, int algo, int min_k, void *stream) {
-    return tmr_xcorr_prec(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze, out,
-                          relu_out, work, out_absmax, tmpl_split, total_rows, algo, min_k, TMR_PREC_F16X3,
-                          stream);
-}
-
-extern "C" int tmr_xcorr(const float *f, int B, int C, int H, int W, const float *templates,
-                         const tmr_unit_t *units, const int32_t *img_units, int U, int max_ht,
-                         int max_wt, const float *scale, int squeeze, float *out, float *relu_out,
-                         float *work, float *out_absmax, void *stream) {
-    return tmr_xcorr_algo(f, B, C, H, W, templates, units, img_units, U, max_ht, max_wt, scale, squeeze,
-                          out, relu_out, work, out_absmax, nullptr, 0, TMR_XCORR_VALU, 1, stream);
 }

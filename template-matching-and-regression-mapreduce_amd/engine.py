@@ -3,10 +3,10 @@
 ``TMREngine`` runs, for a batch of B images x E exemplars (U = B*E matching
 units), everything after the frozen backbone on libtmr.so:
 
-  input_proj (+ upsample x2)     tmr_split_conv_store + tmr_upsample2x   matching_net.py:50-56
+  input_proj (+ upsample x2)     tmr_split_conv + tmr_upsample2x   matching_net.py:50-56
   exemplar templates             tmr_templates       template_matching.py:55-76
-  depthwise xcorr + pad + scale  tmr_xcorr_out       template_matching.py:23-41,97
-  decoders + heads (fused)       tmr_split_conv_heads + tmr_heads_reduce
+  depthwise xcorr + pad + scale  tmr_xcorr           template_matching.py:23-41,97
+  decoders + heads (fused)       tmr_split_conv (heads) + tmr_heads_reduce
                                                      regression_head.py, matching_net.py:63-75
   peaks + decode                 tmr_peaks_decode    TM_utils.py:224-305
   NMS over the exemplar union    tmr_nms             TM_utils.py:307-323, demo.py:106-130
@@ -34,9 +34,9 @@ import torch
 from . import exp_table, host
 from ._lib import (PEAKS_PROB_SCRATCH, PREC_CODES, SPLIT_INIT_BCAST, SPLIT_INIT_BF16, SPLIT_OUT_BF16,
                    SPLIT_TILED_INIT, SPLIT_TILED_OUT, SPLIT_UNITS_PER_IMAGE_SHIFT, SPLIT_XMAX_PER_PIXEL,
-                   SPLIT_XMAX_PER_UNIT,
+                   SPLIT_XMAX_PER_UNIT, SIZE_KINDS, XPACK_ONES, XPACK_UPSAMPLE,
                    UNIT_DTYPE, XCORR_ALGOS, TMRError, call, load, ptr,
-                   require_gpu, stream)
+                   require_gpu, size, stream, xcorr)
 
 NHEAD = 5
 NMS_SMALL = 256  # TMR_NMS_SMALL (include/tmr.h)
@@ -69,7 +69,7 @@ class PathConfig:
                    precision=getattr(args, "precision", "fp32"))
 
 
-# Correlation-kernel crossover (tmr_xcorr_algo).  Since round 3 the table is
+# Correlation-kernel crossover (tmr_xcorr_args_t.algo).  Since round 3 the table is
 # the committed rocprofv3 sweep (xcorr_cost.json, below): kernel-trace
 # durations of both kernels per k in the two regimes, beside each point's
 # counted HBM bytes and MFMA busy (profiles/xcorr_crossover.json; DESIGN.md
@@ -82,13 +82,13 @@ class PathConfig:
 # launch (linear in k in between) and runs the cheaper kernel: at E = 3 the
 # VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
 # crossover); at E = 16 MFMA wins from k = 9 on.  Under the bf16 contract
-# (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr_prec) the MFMA
+# (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr prec) the MFMA
 # kernel wins from k = 5 at E = 3 (profiles/archive/r02af_*).
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
 _T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
     "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
     "mfma": (1.962, 2.577, 3.189, 3.755, 4.350, 4.796, 5.407, 5.987, 6.666, 10.969, 12.070, 13.200, 14.328, 15.542, 16.785, 17.876),
-    # one bf16 term (tmr_xcorr_prec, the bf16 contract), r02af sweep (A prefetch 4 rows)
+    # one bf16 term (tmr_xcorr prec, the bf16 contract), r02af sweep (A prefetch 4 rows)
     "mfma1": (1.875, 2.267, 2.280, 2.634, 2.972, 3.237, 3.465, 3.740, 4.002, 6.008, 6.330, 6.924, 7.386, 7.826, 8.118, 8.554),
 }
 _K192 = (3, 9, 15, 21, 31)
@@ -174,19 +174,6 @@ def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok
     return min(cost, key=cost.get)
 
 
-def xcorr_unit_split(ht: np.ndarray, wt: np.ndarray, units_per_image: float, one_term: bool = False):
-    """Per unit, whether the MFMA correlation is the cheaper kernel for it
-    (the XCORR_COST model at this unit count per image): the unit-level
-    crossover of a launch split by kernel (TMREngine.xcorr_split)."""
-    k = np.maximum(np.asarray(ht), np.asarray(wt)).astype(np.float64)
-    lam = float(np.clip(np.log(max(units_per_image, 1.0) / 3.0) / np.log(16.0 / 3.0), 0.0, 1.0))
-    cost = {}
-    for alg, table in (("valu", "valu"), ("mfma", "mfma1" if one_term else "mfma")):
-        c3, c16 = XCORR_COST[table]
-        cost[alg] = np.interp(k, XCORR_COST_K, (1.0 - lam) * c3 + lam * c16)
-    return cost["mfma"] < cost["valu"]
-
-
 def _version_key(ts: Sequence[torch.Tensor]):
     return tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
 
@@ -210,7 +197,8 @@ class _PackCache:
 
 
 def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """max |x| as a 1-element device tensor (max(out, |x|) when out is given)."""
+    """max |x| as a 1-element device tensor (max(out, |x|) when out is given):
+    tmr_absmax_rows over one row."""
     require_gpu(x, "absmax input")
     if x.dtype != torch.float32:
         raise TMRError(f"absmax of a {x.dtype} tensor (fp32 only)")
@@ -218,7 +206,7 @@ def absmax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     acc = out is not None
     if out is None:
         out = torch.empty(1, device=x.device, dtype=torch.float32)
-    call("tmr_absmax", ptr(x), x.numel(), int(acc), ptr(out), stream())
+    call("tmr_absmax_rows", ptr(x), 1, x.numel(), int(acc), ptr(out), stream())
     return out
 
 
@@ -293,7 +281,7 @@ def pack_split_w(w: torch.Tensor, c0: int, precision: str):
     if ks != ks2:
         raise TMRError("square kernels only (regression_head.py:7)")
     pc = prec_code(precision)
-    n = load().tmr_split_wpack_size(N, c0, C - c0, ks, pc)
+    n = load().tmr_size(SIZE_KINDS["wpack"], N, c0, C - c0, ks, pc, 0)
     if n <= 0:
         raise TMRError(f"unsupported conv shape {tuple(w.shape)}")
     wmax = absmax(w)
@@ -304,13 +292,13 @@ def pack_split_w(w: torch.Tensor, c0: int, precision: str):
 
 def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -> torch.Tensor:
     """[S,C,H,W] fp32 -> zero-padded 16-bit records (tmr_split_xpack); a bf16
-    x (the correlation's bf16 f_TM plane, tmr_xcorr_out) under the bf16
+    x (the correlation's bf16 f_TM plane, tmr_xcorr out_bf16) under the bf16
     contract -> the same records (tmr_split_xpack16).  xmax: one scale source,
     or [S] (one per sample)."""
     require_gpu(x, "conv input")
     S, C, H, W = x.shape
     pc = prec_code(precision)
-    n = load().tmr_split_xpack_size(S, C, H, W, ks, pc)
+    n = load().tmr_size(SIZE_KINDS["xpack"], S, C, H, W, ks, pc, 0)
     if n <= 0:
         raise TMRError(f"unsupported conv input {tuple(x.shape)}")
     out = torch.empty(n, device=x.device, dtype=torch.uint8)
@@ -319,7 +307,7 @@ def pack_split_x(x: torch.Tensor, ks: int, precision: str, xmax: torch.Tensor) -
         call("tmr_split_xpack16", ptr(x), S, C, H, W, ks, pc, ptr(out), stream())
         return out
     x = x.float().contiguous()
-    call("tmr_split_xpack", ptr(x), S, C, H, W, ks, pc, ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
+    call("tmr_split_xpack", ptr(x), S, C, H, W, 0, ks, pc, ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
     return out
 
 
@@ -340,19 +328,20 @@ def fold_proj(w: torch.Tensor, cp: int, proj_w: torch.Tensor, proj_b: torch.Tens
 
 def pack_split_up(f: torch.Tensor, upsample: bool, ks: int, precision: str,
                   xmax: torch.Tensor, ones: bool = True) -> torch.Tensor:
-    """SAM features [S,Cin,h,w] -> records of [up2x(f) or f; 1] (tmr_split_xpack_up;
-    without the constant-1 channel when ones=False)."""
+    """SAM features [S,Cin,h,w] -> records of [up2x(f) or f; 1] (tmr_split_xpack
+    with TMR_XPACK_UPSAMPLE / TMR_XPACK_ONES; without the constant-1 channel
+    when ones=False)."""
     require_gpu(f, "features")
     f = f.float().contiguous()
     S, Cin, Hin, Win = f.shape
     H, W = (2 * Hin, 2 * Win) if upsample else (Hin, Win)
     pc = prec_code(precision)
-    n = load().tmr_split_xpack_size(S, Cin + int(ones), H, W, ks, pc)
+    n = load().tmr_size(SIZE_KINDS["xpack"], S, Cin + int(ones), H, W, ks, pc, 0)
     if n <= 0:
         raise TMRError(f"unsupported feature shape {tuple(f.shape)}")
     out = torch.empty(n, device=f.device, dtype=torch.uint8)
-    call("tmr_split_xpack_up", ptr(f), S, Cin, Hin, Win, int(upsample), int(ones), ks, pc,
-         ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
+    up = (XPACK_UPSAMPLE if upsample else 0) | (XPACK_ONES if ones else 0)
+    call("tmr_split_xpack", ptr(f), S, Cin, Hin, Win, up, ks, pc, ptr(xmax), _per_sample(xmax, S), ptr(out), stream())
     return out
 
 
@@ -373,21 +362,10 @@ def conv2d_split(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, leaky: bool,
     xmax = pixel_absmax(x) if pix else absmax_rows(x)
     xp = pack_split_x(x, ks, precision, xmax)
     out = torch.empty((U, N, H, W), device=x.device, dtype=torch.float32)
-    call("tmr_split_conv_store", ptr(xp), C, None, None, 0, U, H, W, ks, prec_code(precision),
-         ptr(wp), ptr(wmax), ptr(xmax), ptr(b.detach().float().contiguous()), N, int(leaky), None,
+    call("tmr_split_conv", ptr(xp), C, None, None, 0, U, H, W, ks, prec_code(precision),
+         ptr(wp), ptr(wmax), ptr(xmax), ptr(b.detach().float().contiguous()), N, int(leaky), None, None,
          ptr(out), SPLIT_XMAX_PER_PIXEL if pix else SPLIT_XMAX_PER_UNIT, stream())
     return out
-
-
-class FtmRecords:
-    """f_TM as the decoder's bf16 operand records, written by the correlation
-    kernel itself (tmr_xcorr_out's record mode, the bf16 contract's detect
-    path): what TMREngine.decode would otherwise pack f_TM into."""
-
-    def __init__(self, records: torch.Tensor, shape, ks: int):
-        self.records, self.shape, self.ks = records, tuple(shape), ks
-        self.device = records.device
-        self.dtype = torch.bfloat16
 
 
 # graph capture of TMREngine.detect's forward (_DetectGraph): while set, every
@@ -616,33 +594,17 @@ class TMREngine:
         # input channels; same linear map, fp32-level rounding differences)
         self.fold_proj = True
         self._absmax_memo: Dict[tuple, tuple] = {}
-        # correlation kernel: "auto" (the crossover rule in tmr_xcorr_algo),
-        # "valu" or "mfma" (csrc/xcorr.hip)
+        # correlation kernel: "auto" (the crossover rule, XCORR_COST), "valu" or
+        # "mfma" (csrc/xcorr.hip).  (Round 5's per-unit split of a mixed launch
+        # over two streams, its in-kernel A fragments and its bf16 record output
+        # were measured, not kept and removed in round 6: DESIGN_HISTORY.md.)
         self.xcorr_algo = "auto"
         self.last_xcorr_algo = None
-        # "auto" correlation of a mixed launch split by kernel per unit: the
-        # units the MFMA kernel wins on run it, the others the VALU kernel,
-        # the two launches on two streams (subset launches: tmr_unit_t.out_unit).
-        # "auto": only when images hold about one unit each -- with several
-        # units per image the split loses the band staging they share
-        # (measured, profiles/archive/r05/r05b/xcorr_split_ab.json: config B 5.09 -> 5.38 ms,
-        # C 2.99 -> 3.56, E equal; D, one unit per image, 2.38 -> 2.19 ms)
-        self.xcorr_split = "auto"
-        self._side = None
-        # the MFMA correlation's template operands: "split" (tmr_template_split
-        # pre-expands the A fragments in HBM) or "lds" (the kernel builds them
-        # from the LDS-staged template; bit-identical)
-        self.xcorr_afrag = os.environ.get("TMR_XCORR_AFRAG", "split")
         self.last_nms_small = False  # detect: the kept rows came from the in-forward small NMS
         # bf16 contract, detect path: the one-term MFMA correlation writes
         # f_TM as bf16 (the decoder's bf16 records are bf16(f_TM) either way)
         self.out_bf16 = True
         self.last_xcorr_out16 = False
-        # ... or as the decoder's records themselves (no plane, no record pass):
-        # off by default -- each block is one channel, so a record's 16 B come
-        # from 8 blocks as 2-B stores: config C correlation 3.7 -> 8.0 ms, step
-        # 53.3 -> 56.7 ms against the plane + record pass (profiles/archive/r05/r05g)
-        self.out_records = os.environ.get("TMR_XCORR_RECORDS", "0") == "1"
         # keep an image's projection and decoder fp half for the next call on
         # the same feature tensor (the module API's per-exemplar calls)
         self.reuse_image_work = False
@@ -743,10 +705,10 @@ class TMREngine:
             one = torch.ones(1, device=dev, dtype=torch.float32)
             xp = pack_split_x(ones, ks, prec, one)
             wp, wmax = pack_split_w(wbias, 1, prec)
-            plane = torch.empty(load().tmr_split_acc_size(1, N, H, W), device=dev, dtype=torch.float32)
+            plane = torch.empty(size("acc", 1, N, H, W), device=dev, dtype=torch.float32)
             zero = torch.zeros(N, device=dev, dtype=torch.float32)
-            call("tmr_split_conv_store", ptr(xp), 1, None, None, 0, 1, H, W, ks, prec_code(prec),
-                 ptr(wp), ptr(wmax), ptr(one), ptr(zero), N, 0, None, ptr(plane),
+            call("tmr_split_conv", ptr(xp), 1, None, None, 0, 1, H, W, ks, prec_code(prec),
+                 ptr(wp), ptr(wmax), ptr(one), ptr(zero), N, 0, None, None, ptr(plane),
                  SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if self._plane16() else 0), stream())
             return plane
 
@@ -826,13 +788,13 @@ class TMREngine:
         # (input_proj(up2x(f)) and up2x(input_proj(f)) differ in fp32
         # rounding only)
         Hq, Wq = Hin, Win
-        n = load().tmr_split_xpack_size(B, Cin, Hq, Wq, 1, pcode)
+        n = size("xpack", B, Cin, Hq, Wq, 1, pcode)
         xp = torch.empty(n, device=feats.device, dtype=torch.uint8)
-        call("tmr_split_xpack_up", ptr(feats), B, Cin, Hin, Win, 0, 0, 1, pcode,
+        call("tmr_split_xpack", ptr(feats), B, Cin, Hin, Win, 0, 1, pcode,
              ptr(xmax), _per_sample(xmax, B), ptr(xp), stream())
         fq = torch.empty((B, N, Hq, Wq), device=feats.device, dtype=torch.float32)
-        call("tmr_split_conv_store", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
-             ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, ptr(fq),
+        call("tmr_split_conv", ptr(xp), Cin, None, None, 0, B, Hq, Wq, 1, pcode, ptr(wp),
+             ptr(wmax), ptr(xmax), ptr(pb.detach().float().contiguous()), N, 0, None, None, ptr(fq),
              SPLIT_XMAX_PER_PIXEL if xmax is not None else 0, stream())
         if up:
             fp = torch.empty((B, N, H, W), device=feats.device, dtype=torch.float32)
@@ -849,11 +811,11 @@ class TMREngine:
         return fp, f0
 
     def match(self, fp: torch.Tensor, unit_image: Sequence[int], unit_boxes: np.ndarray,
-              want_relu: bool = False, allow_bf16: bool = False, records_ks: Optional[int] = None):
+              want_relu: bool = False, allow_bf16: bool = False):
         """TemplateMatching.forward over units -> f_TM [U,C|1,H,W] (+ relu).
         allow_bf16: the caller only packs f_TM into bf16 decoder records (the
         bf16 contract's detect path), so the one-term bf16 MFMA kernel may
-        write it as bf16 (tmr_xcorr_out; the records are bit-identical)."""
+        write it as bf16 (tmr_xcorr out_bf16; the records are bit-identical)."""
         B, C, H, W = fp.shape
         U = len(unit_image)
         cfg = self.cfg
@@ -885,42 +847,21 @@ class TMREngine:
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice
         algo = XCORR_ALGOS[choice]
-        split = None
-        upi = U / max(1, len(set(unit_image)))
-        want_split = self.xcorr_split is True or (self.xcorr_split == "auto" and upi < 1.5)
-        if want_split and self.xcorr_algo == "auto" and fits and not cfg.squeeze and \
-                getattr(_capture, "blob", None) is None and U > 1:
-            mf = xcorr_unit_split(units["ht"], units["wt"], U / max(1, len(set(unit_image))),
-                                  one_term=pc != PREC_CODES["fp32"])
-            if mf.any() and not mf.all():
-                split = mf
-                choice = "split"
-                self.last_xcorr_algo = choice
         out16 = (allow_bf16 and self.out_bf16 and pc == PREC_CODES["bf16"] and algo == XCORR_ALGOS["mfma"]
-                 and not cfg.squeeze and not want_relu and W % 8 == 0 and split is None)
+                 and not cfg.squeeze and not want_relu and W % 8 == 0)
         self.last_xcorr_out16 = out16
-        rec = out16 and records_ks is not None and self.out_records and C % 32 == 0
-        if rec:  # the decoder's bf16 records straight from the correlation epilogue
-            n = load().tmr_split_xpack_size(U, C, H, W, records_ks, pc)
-            out = torch.empty(n, device=dev, dtype=torch.uint8)
-            call("tmr_split_xpack_ring", ptr(out), U, C, H, W, records_ks, pc, stream())
-        else:
-            out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
+        out = torch.empty((U, Co, H, W), device=dev, dtype=torch.bfloat16 if out16 else torch.float32)
         relu = torch.empty_like(out) if want_relu else None
-        tsplit = None
-        if split is not None:
-            self._match_split(fp, tmpl, units, unit_image, split, scale, out, relu, slots, pc)
-        else:
-            if algo != XCORR_ALGOS["valu"] and tfl > 0 and not self._lds_afrag(pc):
-                # the MFMA correlation's template operands (per (unit, channel) scale)
-                rows = host.tsplit_rows(units)
-                tsplit = torch.empty(load().tmr_template_split_size(U, C, rows), device=dev, dtype=torch.uint8)
-                call("tmr_template_split_prec", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
-            call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(units_d), ptr(img_units_d), U, mh,
-                 mw, ptr(scale), int(cfg.squeeze), ptr(out), ptr(relu) if relu is not None else None,
-                 ptr(work) if work is not None else None, ptr(slots),
-                 ptr(tsplit) if tsplit is not None else None, rows if tsplit is not None else 0, algo, min_k, pc,
-                 (2 + records_ks) if rec else int(out16), stream())
+        tsplit, rows = None, 0
+        if algo != XCORR_ALGOS["valu"] and tfl > 0:
+            # the MFMA correlation's template operands (per (unit, channel) scale)
+            rows = host.tsplit_rows(units)
+            tsplit = torch.empty(size("template_split", U, C, rows), device=dev, dtype=torch.uint8)
+            call("tmr_template_split", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
+        xcorr(f=ptr(fp), templates=ptr(tmpl), units=ptr(units_d), img_units=ptr(img_units_d), scale=ptr(scale),
+              out=ptr(out), relu_out=ptr(relu), work=ptr(work), out_absmax=ptr(slots), tmpl_split=ptr(tsplit),
+              total_rows=rows, B=B, C=C, H=H, W=W, U=U, max_ht=mh, max_wt=mw, squeeze=int(cfg.squeeze),
+              algo=algo, min_k=min_k, prec=pc, out_bf16=int(out16), stream=stream())
         if ev is not None:
             ev[1].record()
             self.xcorr_events.append(ev)
@@ -934,69 +875,9 @@ class TMREngine:
         # write one f_TM plane per unit
         # (fp32 reads; the f_TM write is bf16, 2 B, under out16)
         nimg = len(set(int(i) for i in unit_image))
-        if split is not None:  # each launch stages the planes of its own units' images
-            ui_ = np.asarray(unit_image)
-            nimg = len(set(ui_[split].tolist())) + len(set(ui_[~split].tolist()))
         self.last_xcorr_dram_bytes = float(C * H * W) * (4.0 * nimg + (2.0 if out16 else 4.0) * U)
-        if rec:
-            return FtmRecords(out, (U, Co, H, W), records_ks), relu
         self._memo_absmax(out, "ftm", lambda: slots)
         return out, relu
-
-    def _lds_afrag(self, pc: int) -> bool:
-        """The MFMA correlation builds its A fragments in-kernel (3-term only)."""
-        return self.xcorr_afrag == "lds" and pc == PREC_CODES["fp32"]
-
-    def _match_split(self, fp, tmpl, units, unit_image, mfma_units, scale, out, relu, slots, pc):
-        """The correlation as two launches over complementary unit subsets
-        (each unit's output plane / max slot / exponent row = its out_unit):
-        the MFMA kernel's units on the current stream, the VALU kernel's on a
-        side stream (joined back before anything reads f_TM), so the two
-        kernels' blocks share the chip instead of one kernel running units it
-        is slower on."""
-        B, C, H, W = fp.shape
-        dev = fp.device
-        ui = np.asarray(unit_image, np.int64)
-        main = torch.cuda.current_stream(dev)
-        if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(device=dev)
-        side = self._side
-        fork = torch.cuda.Event()
-        fork.record(main)
-        subs = []
-        for is_mfma in (False, True):
-            idx = np.nonzero(mfma_units == is_mfma)[0]
-            sub = units[idx].copy()
-            sub_ui = ui[idx]
-            subs.append((is_mfma, sub, sub_ui))
-        rows = host.tsplit_rows(units)  # absolute row offsets: the full set's buffer
-        lds_a = self._lds_afrag(pc)  # (the kernel builds its A fragments)
-        tsplit = None if lds_a else \
-            torch.empty(load().tmr_template_split_size(len(units), C, rows), device=dev, dtype=torch.uint8)
-        for is_mfma, sub, sub_ui in subs:
-            st = main if is_mfma else side
-            with torch.cuda.stream(st):
-                if not is_mfma:
-                    st.wait_event(fork)
-                sub_d = _units_to_device(sub, dev)
-                iu_d = _h2d(host.image_ranges(sub_ui, B), dev)
-                mh, mw = int(sub["ht"].max()), int(sub["wt"].max())
-                min_k = int(min(sub["ht"].min(), sub["wt"].min()))
-                if is_mfma and tsplit is not None:
-                    call("tmr_template_split_prec", ptr(tmpl), ptr(sub_d), len(sub), C, rows, pc, ptr(tsplit),
-                         stream())
-                call("tmr_xcorr_out", ptr(fp), B, C, H, W, ptr(tmpl), ptr(sub_d), ptr(iu_d), len(sub), mh, mw,
-                     ptr(scale), 0, ptr(out), ptr(relu) if relu is not None else None, None, ptr(slots),
-                     ptr(tsplit) if is_mfma and tsplit is not None else None,
-                     rows if is_mfma and tsplit is not None else 0,
-                     XCORR_ALGOS["mfma" if is_mfma else "valu"], min_k, pc, 0, stream())
-        join = torch.cuda.Event()
-        join.record(side)
-        main.wait_event(join)
-        # the side stream's buffers are used across streams: keep them alive
-        # until the main stream has passed the join
-        for t in (fp, tmpl, out, slots) + tuple(x for x in (tsplit, relu) if x is not None):
-            t.record_stream(side)
 
     def decode(self, fp: torch.Tensor, f_tm: torch.Tensor, unit_image: Sequence[int],
                feats: Optional[torch.Tensor] = None):
@@ -1034,7 +915,7 @@ class TMREngine:
             if fold:  # the fp half runs on up2x(f) (Cin channels) + the bias plane
                 C0 = feats.shape[1]
                 bplane = self._bias_plane(wbias, H, W)
-            nparts = load().tmr_heads_partials_size(N, U, H, W)
+            nparts = size("heads_partials", N, U, H, W)
             part = torch.empty(nparts, device=dev, dtype=torch.float32)
             acc0 = None
             C0k = C0
@@ -1050,7 +931,7 @@ class TMREngine:
                 # convex), per image
                 xmax0 = self._feat_absmax(feats)
                 if share:
-                    # the fp half is its own launch (tmr_split_conv_store) with
+                    # the fp half is its own launch (tmr_split_conv, tiled out) with
                     # its own per-image scales
                     xmax1 = tm_max
                     acc0 = self._acc0_lookup(feats, split, H, W)
@@ -1061,7 +942,7 @@ class TMREngine:
                     # per image, max(max|f|, max|f_TM| of its units)
                     xs0, xmax1 = (None, None) if unscaled else scale_merge(xmax0, tm_max, ui, B)
                     xp0 = pack_split_up(feats, cfg.feature_upsample, ks, cfg.precision, xs0, ones=False)
-                xp1 = f_tm.records if isinstance(f_tm, FtmRecords) else pack_split_x(f_tm, ks, cfg.precision, xmax1)
+                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
                 C0k = C0
             else:
                 if share:
@@ -1073,18 +954,17 @@ class TMREngine:
                     xp0 = pack_split_x(fp, ks, cfg.precision, xs0)
                 else:
                     xp0, xmax1 = None, tm_max
-                xp1 = f_tm.records if isinstance(f_tm, FtmRecords) else pack_split_x(f_tm, ks, cfg.precision, xmax1)
+                xp1 = pack_split_x(f_tm, ks, cfg.precision, xmax1)
             xpu = 0 if unscaled else SPLIT_XMAX_PER_UNIT
             if share:
                 wp_fp, wp_tm, zero_b = split
                 if acc0 is None:  # acc0 in the kernel's tiled accumulator layout (private)
-                    acc0 = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=dev,
-                                       dtype=torch.float32)
+                    acc0 = torch.empty(size("acc", B, N, H, W), device=dev, dtype=torch.float32)
                     fl = SPLIT_TILED_OUT | (SPLIT_OUT_BF16 if acc16 else 0) | xpu
                     if bplane is not None:
                         fl |= SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
-                    call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
-                         ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0,
+                    call("tmr_split_conv", ptr(xp0), C0, None, None, 0, B, H, W, ks, pc,
+                         ptr(wp_fp[0]), ptr(wp_fp[1]), ptr(xmax0), ptr(zero_b), N, 0, None,
                          ptr(bplane) if bplane is not None else None, ptr(acc0), fl, stream())
                     if fold and self.reuse_image_work:
                         self._acc0_store(feats, split, H, W, acc0)
@@ -1100,7 +980,7 @@ class TMREngine:
                 a0 = ptr(bplane)
                 fl = SPLIT_TILED_INIT | SPLIT_INIT_BCAST | (SPLIT_INIT_BF16 if self._plane16() else 0)
             fl |= xpu | (self._units_per_image(unit_image, B) << SPLIT_UNITS_PER_IMAGE_SHIFT)
-            call("tmr_split_conv_heads", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
+            call("tmr_split_conv", ptr(xp0) if C0k else None, C0k, ptr(ui), ptr(xp1), C1,
                  U, H, W, ks, pc, ptr(wp[0]), ptr(wp[1]), ptr(xmax1), ptr(bias), N, 1, ptr(hw),
                  a0, ptr(part), fl, stream())
             if ev is not None:
@@ -1291,8 +1171,7 @@ class TMREngine:
             # records and nothing else reads it
             split1 = self.cfg.decoder_num_layer == 1
             f_tm, relu = self.match(fp, unit_image, np.asarray(unit_boxes, np.float32), want_aux,
-                                    allow_bf16=split1 and not want_aux,
-                                    records_ks=self.cfg.decoder_kernel_size if split1 and not want_aux else None)
+                                    allow_bf16=split1 and not want_aux)
         o, b = self.decode(fp, f_tm, unit_image, feats)
         return dict(o=o, b=b, f_tm_relu=relu, f0=f0, fp=fp)
 
@@ -1343,7 +1222,7 @@ class TMREngine:
         cand_off, nb_off, max_cand = host.nms_offsets(counts_host, seg_units)
         T = int(cand_off[-1])
         sum_nb = int(nb_off[-1])
-        work = torch.empty(max(load().tmr_nms_work_size(T, sum_nb, max_cand, G), 1), device=dev,
+        work = torch.empty(max(size("nms_work", T, sum_nb, max_cand, G), 1), device=dev,
                            dtype=torch.uint8)
         parts = [np.asarray(seg_units, np.int32), np.asarray(cand_off, np.int64), np.asarray(nb_off, np.int64)]
         if counts is None:

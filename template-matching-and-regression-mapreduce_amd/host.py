@@ -143,7 +143,6 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         units["tmpl_offset"] = np.concatenate([[0], np.cumsum(sizes)[:-1]])
         rows = ht * tsplit_nk_vec(wt)
         units["row_offset"] = np.concatenate([[0], np.cumsum(rows)[:-1]])
-        units["out_unit"] = np.arange(U, dtype=np.int32)
         return units, int(sizes.sum()), max(1, int(ht.max())), max(1, int(wt.max()))
     # per unit (prototype templates, and few units: the module API's one
     # exemplar per call, where the vector form's per-call overhead dominates)
@@ -157,7 +156,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         else:
             pbox = tuple(prototype_box(boxes[u], H, W).tolist())
             roi, ht, wt = (0.0, 0.0, 0.0, 0.0), 1, 1
-        units[u] = (int(images[u]), ttype, ht, wt, roi, pbox, off, rows, u)
+        units[u] = (int(images[u]), ttype, ht, wt, roi, pbox, off, rows, 0)
         off += C * ht * wt
         rows += ht * tsplit_nk(wt)
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)

@@ -4,10 +4,10 @@
 Same constructors, reference initialisation (N(0, 0.01) weights, zero bias,
 :17-24) and state_dict keys (``layer.<2i>.weight``, ``head.0.weight``).
 ``Decoder_model`` runs on the split 16-bit-MFMA implicit-GEMM kernel
-(tmr_split_conv_store; ``precision`` "fp32" = 3-term fp16 split, the fp32
+(tmr_split_conv; ``precision`` "fp32" = 3-term fp16 split, the fp32
 1e-5 contract; "bf16" = config C), the 1x1 heads on the same kernel at
 ks = 1 (3-term split, fp32 contract).  Inside ``matching_net`` the decoders
-and heads are not called one by one: the fused kernel (tmr_split_conv_heads)
+and heads are not called one by one: the fused kernel (tmr_split_conv with heads)
 consumes their parameters directly.
 """
 from __future__ import annotations

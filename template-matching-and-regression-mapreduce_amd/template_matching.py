@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from . import host
-from ._lib import UNIT_DTYPE, TMRError, call, ptr, require_gpu, stream
+from ._lib import PREC_CODES, UNIT_DTYPE, XCORR_ALGOS, TMRError, call, ptr, require_gpu, stream, xcorr
 from .engine import PathConfig, TMREngine, _h2d, _units_to_device
 
 
@@ -141,10 +141,9 @@ class TemplateMatching(nn.Module):
         if scale is None:
             scale = torch.ones(1, device=sample.device, dtype=torch.float32)
         eng = TMREngine({"matcher.scale": scale}, cfg)
-        # one kernel for the whole launch (no per-unit split): the batched
-        # matcher then equals its own cross_correlation member bit for bit
-        # when the cost model picks the VALU kernel, as the member runs
-        eng.xcorr_split = False
+        # one kernel for the whole launch: the batched matcher equals its own
+        # cross_correlation member bit for bit when the cost model picks the
+        # VALU kernel, as the member runs
         out, _ = eng.match(sample.float().contiguous(), list(range(B)), boxes)
         return out
 
@@ -172,13 +171,13 @@ def _xcorr(feature: torch.Tensor, template: torch.Tensor, scale: torch.Tensor,
     units["ht"], units["wt"] = h, w
     units["tmpl_offset"] = np.arange(bs) * (C * h * w)
     units["row_offset"] = np.arange(bs) * h * host.tsplit_nk(w)
-    units["out_unit"] = np.arange(bs)
     dev = feature.device
     ud = _units_to_device(units, dev)
     iu = _h2d(np.arange(bs + 1, dtype=np.int32), dev)
     out = torch.empty((bs, 1 if squeeze else C, H, W), device=dev, dtype=torch.float32)
     work = torch.empty((bs, C, H, W), device=dev, dtype=torch.float32) if squeeze else None
-    call("tmr_xcorr", ptr(feature), bs, C, H, W, ptr(template), ptr(ud), ptr(iu), bs, h, w,
-         ptr(scale.detach().float().contiguous()), int(squeeze), ptr(out), None,
-         ptr(work) if work is not None else None, None, stream())
+    xcorr(f=ptr(feature), templates=ptr(template), units=ptr(ud), img_units=ptr(iu),
+          scale=ptr(scale.detach().float().contiguous()), out=ptr(out), work=ptr(work), B=bs, C=C, H=H, W=W,
+          U=bs, max_ht=h, max_wt=w, squeeze=int(squeeze), algo=XCORR_ALGOS["valu"], min_k=1,
+          prec=PREC_CODES["fp32"], stream=stream())
     return out

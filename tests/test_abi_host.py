@@ -29,7 +29,10 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes table out of sync with tmr.h"
     L = tmr_amd.load()
-    assert L.tmr_version() == 2
+    assert L.tmr_version() == 3
+    # ABI 3: one correlation entry point, one sizing query, one
+    # split conv entry point -- at most ~25 symbols
+    assert len(syms) <= 25, syms
     assert L.tmr_strerror(0) == b"ok"
     assert b"invalid" in L.tmr_strerror(-1)
 
@@ -39,17 +42,26 @@ def test_struct_layouts():
     assert _lib.PEAK_DTYPE.itemsize == 24
 
 
+def _size(kind, *d):
+    return int(tmr_amd.load().tmr_size(_lib.SIZE_KINDS[kind], *(list(d) + [0] * (6 - len(d)))))
+
+
 def test_size_queries_no_gpu():
-    L = tmr_amd.load()
-    assert L.tmr_heads_partials_size(2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
-    assert L.tmr_nms_work_size(10, 4, 5, 3) > 10 * 40
+    assert _size("heads_partials", 2048, 3, 8, 8) == 32 * 5 * 3 * 64  # 64-wide tiles
+    assert _size("nms_work", 10, 4, 5, 3) > 10 * 40
     # linear in the candidates (the binned NMS keeps no n^2 IoU matrix): at most
     # 640 B per candidate (a 128-entry suppressor list is 512 of them) plus a
     # fixed part, 64 images x 49,152 candidates
-    big = L.tmr_nms_work_size(64 * 49152, 64 * 768, 49152, 64)
+    big = _size("nms_work", 64 * 49152, 64 * 768, 49152, 64)
     assert big < 64 * 49152 * 640 + (16 << 20)
-    half = L.tmr_nms_work_size(32 * 49152, 32 * 768, 49152, 32)
+    half = _size("nms_work", 32 * 49152, 32 * 768, 49152, 32)
     assert abs(big - 2 * half) < (4 << 20)
+    # the documented worst case (include/tmr.h): one image of 589,824 candidates
+    assert _size("nms_work", 589824, 589824 // 64, 589824, 1) < 0.4e9
+    assert _size("template_split", 3, 512, 45) == 512 * 45 * 2 * 1024 + 4 * 3 * 512
+    assert _size("stats_work", 4) > 0
+    assert tmr_amd.load().tmr_size(99, 1, 1, 1, 1, 1, 1) == -1  # unknown kind
+    assert _size("acc", 1 << 40, 8, 8, 8) == -1  # dimensions past int range
 
 
 def test_split_size_queries_no_gpu():
@@ -57,15 +69,14 @@ def test_split_size_queries_no_gpu():
     padded to whole 16x32 tiles plus the ks halo, one 64-B record per pixel per
     32-channel chunk and half (fp32 3-term: hi and lo halves); weights
     [ks^2][chunks][ceil(N/128)*128][128 B (wh, wl) | 64 B]."""
-    L = tmr_amd.load()
-    assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 0) == 2 * 32 * 130 * 130 * 64
-    assert L.tmr_split_xpack_size(2, 512, 128, 128, 3, 1) == 2 * 16 * 130 * 130 * 64
-    assert L.tmr_split_xpack_size(1, 257, 17, 33, 1, 0) == 1 * 9 * 2 * 32 * 64 * 64
-    assert L.tmr_split_xpack_size(1, 8, 8, 8, 4, 0) == -1   # even kernel
-    assert L.tmr_split_xpack_size(1, 8, 8, 8, 3, 5) == -1   # unknown precision
-    assert L.tmr_split_wpack_size(2048, 257, 512, 3, 0) == 9 * (9 + 16) * 2048 * 128
-    assert L.tmr_split_wpack_size(100, 0, 40, 5, 2) == 25 * 2 * 128 * 64
-    assert L.tmr_split_wpack_size(8, 0, 0, 3, 0) == -1
+    assert _size("xpack", 2, 512, 128, 128, 3, 0) == 2 * 32 * 130 * 130 * 64
+    assert _size("xpack", 2, 512, 128, 128, 3, 1) == 2 * 16 * 130 * 130 * 64
+    assert _size("xpack", 1, 257, 17, 33, 1, 0) == 1 * 9 * 2 * 32 * 64 * 64
+    assert _size("xpack", 1, 8, 8, 8, 4, 0) == -1   # even kernel
+    assert _size("xpack", 1, 8, 8, 8, 3, 5) == -1   # unknown precision
+    assert _size("wpack", 2048, 257, 512, 3, 0) == 9 * (9 + 16) * 2048 * 128
+    assert _size("wpack", 100, 0, 40, 5, 2) == 25 * 2 * 128 * 64
+    assert _size("wpack", 8, 0, 0, 3, 0) == -1
 
 
 def test_invalid_arguments_return_codes():
@@ -75,18 +86,23 @@ def test_invalid_arguments_return_codes():
     # the compact reference-exp table: a malformed blob is refused
     junk = np.zeros(64, np.uint8)
     assert L.tmr_exp_table_decode(junk.ctypes.data, junk.size, None, 0) == -1
-    assert L.tmr_xcorr(None, 1, 1, 1, 1, None, None, None, 1, 1, 1, None, 0, None, None, None, None,
-                       None) == -1
+    assert L.tmr_xcorr(None, None) == -1
+    args = _lib.XcorrArgs()
+    args.B = args.C = args.H = args.W = args.U = args.max_ht = args.max_wt = 1
+    assert L.tmr_xcorr(ctypes.byref(args), None) == -1  # NULL tensors
+    assert ctypes.sizeof(_lib.XcorrArgs) == 10 * 8 + 8 + 12 * 4  # tmr_xcorr_args_t
     assert L.tmr_nms(*([None] * 8), 0, 0, 0, 0, 0.5, *([None] * 7)) == -1
     # split conv: bad precision / kernel size / missing scale sources never launch
-    assert L.tmr_split_conv_store(None, 0, None, None, 8, 1, 8, 8, 3, 9, None, None, None, None, 8, 0,
-                                  None, None, 0, None) == -1
-    assert L.tmr_split_conv_heads(None, 0, None, None, 8, 1, 8, 8, 2, 0, None, None, None, None, 8, 1,
-                                  None, None, None, 0, None) == -1
-    assert L.tmr_split_acc_size(2, 2048, 128, 128) == 2 * 2048 * 128 * 128
-    assert L.tmr_split_acc_size(1, 100, 17, 33) == 128 * 32 * 64
-    assert L.tmr_split_xpack(None, 1, 8, 8, 8, 3, 0, None, 0, None, None) == -1
-    assert L.tmr_absmax(None, 4, 0, None, None) == -1
+    assert L.tmr_split_conv(None, 0, None, None, 8, 1, 8, 8, 3, 9, None, None, None, None, 8, 0,
+                            None, None, None, 0, None) == -1
+    assert L.tmr_split_conv(None, 0, None, None, 8, 1, 8, 8, 2, 0, None, None, None, None, 8, 1,
+                            None, None, None, 0, None) == -1
+    assert _size("acc", 2, 2048, 128, 128) == 2 * 2048 * 128 * 128
+    assert _size("acc", 1, 100, 17, 33) == 128 * 32 * 64
+    assert L.tmr_split_xpack(None, 1, 8, 8, 8, 0, 3, 0, None, 0, None, None) == -1
+    buf8 = np.zeros(8, np.float32)
+    assert L.tmr_split_xpack(buf8.ctypes.data, 1, 8, 8, 8, 4, 3, 0, buf8.ctypes.data, 0, buf8.ctypes.data,
+                             None) == -1  # unknown `up` bit
     # per-sample scale sources (ABI 2): missing pointers / empty batches never launch
     assert L.tmr_absmax_rows(None, 2, 4, 0, None, None) == -1
     assert L.tmr_absmax_rows(None, 0, 4, 0, None, None) == -1
@@ -323,7 +339,7 @@ def test_build_units_vectorised_matches_scalar():
         assert (units["ht"][u], units["wt"][u]) == (ht, wt)
         assert np.array_equal(units["roi"][u].view(np.uint32), roi.view(np.uint32))
         assert units["tmpl_offset"][u] == off and units["row_offset"][u] == rows
-        assert units["out_unit"][u] == u
+        assert units["pad_"][u] == 0
         off += C * ht * wt
         rows += ht * host.tsplit_nk(wt)
     assert tfl == off and mh == units["ht"].max() and mw == units["wt"].max()
@@ -339,7 +355,6 @@ def test_build_units_vectorised_matches_scalar():
         ref = units[u0:u0 + n].copy()
         ref["tmpl_offset"] -= ref["tmpl_offset"][0]
         ref["row_offset"] -= ref["row_offset"][0]
-        ref["out_unit"] -= ref["out_unit"][0]
         for f in small.dtype.names:  # field-wise (a structured copy leaves the padding undefined)
             a, b = np.ascontiguousarray(small[f]), np.ascontiguousarray(ref[f])
             assert a.tobytes() == b.tobytes(), (u0, n, f)

@@ -107,7 +107,7 @@ def test_xcorr_golden(golden):
         # drive tmr_xcorr directly with the golden template (no RoIAlign)
         units = np.zeros(1, tmr_amd._lib.UNIT_DTYPE)
         units["ht"], units["wt"], units["tmpl_offset"] = h, w, 0
-        from tmr_amd._lib import call, ptr, stream
+        from tmr_amd._lib import PREC_CODES, XCORR_ALGOS, ptr, stream, xcorr
         from tmr_amd.engine import _units_to_device
         fd, td = cuda(f), cuda(t.reshape(-1))
         out = torch.empty((1, 1 if sq else C, H, W), device=DEV)
@@ -117,8 +117,9 @@ def test_xcorr_golden(golden):
         ud = _units_to_device(units, DEV)
         iu = cuda(np.array([0, 1], np.int32))
         amax = torch.zeros(1, device=DEV)  # per-unit max |f_TM| (one unit)
-        call("tmr_xcorr", ptr(fd), 1, C, H, W, ptr(td), ptr(ud), ptr(iu), 1, h, w, ptr(scale), sq,
-             ptr(out), ptr(relu), ptr(work) if work is not None else None, ptr(amax), stream())
+        xcorr(f=ptr(fd), templates=ptr(td), units=ptr(ud), img_units=ptr(iu), scale=ptr(scale), out=ptr(out),
+              relu_out=ptr(relu), work=ptr(work), out_absmax=ptr(amax), B=1, C=C, H=H, W=W, U=1, max_ht=h,
+              max_wt=w, squeeze=sq, algo=XCORR_ALGOS["valu"], min_k=1, prec=PREC_CODES["fp32"], stream=stream())
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert normwise(got, ref) <= TOL, (i, normwise(got, ref))
@@ -201,7 +202,7 @@ SPLIT_TOL = {"fp32": TOL, "f16": 1e-3, "bf16": 1e-2}
                                               (16, 16, 24, 24, 5, True), (24, 8, 20, 20, 1, False),
                                               (12, 12, 9, 9, 7, True), (512, 2048, 16, 16, 3, True)])
 def test_split_conv_vs_torch(C, N, H, W, ks, leaky, prec):
-    """Split 16-bit MFMA kernel (tmr_split_conv_store) vs ATen conv2d (fp32
+    """Split 16-bit MFMA kernel (tmr_split_conv) vs ATen conv2d (fp32
     CPU) with an acc_init input: "fp32" (3-term fp16 split) within the 1e-5
     contract, one-term bf16 / f16 within their stated tolerances."""
     from tmr_amd._lib import PREC_CODES, call, ptr, stream
@@ -219,8 +220,8 @@ def test_split_conv_vs_torch(C, N, H, W, ks, leaky, prec):
     xmax = absmax(xd)
     xp = pack_split_x(xd, ks, prec, xmax)
     out = torch.empty((2, N, H, W), device=DEV)
-    call("tmr_split_conv_store", ptr(xp), C, None, None, 0, 2, H, W, ks, PREC_CODES[prec], ptr(wp),
-         ptr(wmax), ptr(xmax), ptr(bd), N, int(leaky), ptr(initd), ptr(out), 0, stream())
+    call("tmr_split_conv", ptr(xp), C, None, None, 0, 2, H, W, ks, PREC_CODES[prec], ptr(wp),
+         ptr(wmax), ptr(xmax), ptr(bd), N, int(leaky), None, ptr(initd), ptr(out), 0, stream())
     torch.cuda.synchronize()
     assert normwise(out.cpu().numpy(), ref.numpy()) <= SPLIT_TOL[prec]
 
@@ -229,7 +230,7 @@ def test_split_conv_vs_torch(C, N, H, W, ks, leaky, prec):
 def test_split_conv_scales_and_two_sources(scale):
     """Activations far from unit scale (the power-of-two split scale), zero
     rows, and the two-source virtual concat (src0 per image via unit_image,
-    src1 per unit) of tmr_split_conv_heads vs the unsplit fp32 reference."""
+    src1 per unit) of tmr_split_conv (heads) vs the unsplit fp32 reference."""
     from tmr_amd._lib import call, ptr, stream
     from tmr_amd.engine import absmax, pack_split_w, pack_split_x
     torch.manual_seed(3)
@@ -252,8 +253,8 @@ def test_split_conv_scales_and_two_sources(scale):
     xmax = absmax(d["x1"], absmax(d["x0"]))
     xp0 = pack_split_x(d["x0"], 3, "fp32", xmax)
     xp1 = pack_split_x(d["x1"], 3, "fp32", xmax)
-    part = torch.empty(tmr_amd._lib.load().tmr_heads_partials_size(N, U, H, W), device=DEV)
-    call("tmr_split_conv_heads", ptr(xp0), C0, ptr(uid), ptr(xp1), C1, U, H, W, 3, 0, ptr(wp),
+    part = torch.empty(tmr_amd._lib.size("heads_partials", N, U, H, W), device=DEV)
+    call("tmr_split_conv", ptr(xp0), C0, ptr(uid), ptr(xp1), C1, U, H, W, 3, 0, ptr(wp),
          ptr(wmax), ptr(xmax), ptr(d["b"]), N, 1, ptr(d["hw"]), None, ptr(part), 0, stream())
     o = torch.empty((U, 1, H, W), device=DEV)
     bb = torch.empty((U, 4, H, W), device=DEV)
@@ -324,7 +325,7 @@ def test_xpack_records_bitexact(S, C, H, W, ks):
     """Activation records (the 4-pixel kernel for W % 4 == 0, the one-pixel
     kernel otherwise) bit-exact against the torch restatement of the layout,
     padding ring included (the buffer is pre-filled with garbage)."""
-    from tmr_amd._lib import PREC_CODES, call, load, ptr, stream
+    from tmr_amd._lib import PREC_CODES, call, ptr, size, stream
     from tmr_amd.engine import absmax, absmax_rows, pixel_absmax
     torch.manual_seed(11)
     # samples 2^20 apart and a quiet pixel block: the per-sample and per-pixel
@@ -334,9 +335,10 @@ def test_xpack_records_bitexact(S, C, H, W, ks):
     x = x.cuda()
     for mode, xmax in ((0, absmax(x)), (1, absmax_rows(x)), (2, pixel_absmax(x))):
         for prec in ("fp32", "bf16", "f16"):
-            n = load().tmr_split_xpack_size(S, C, H, W, ks, PREC_CODES[prec])
+            n = size("xpack", S, C, H, W, ks, PREC_CODES[prec])
             out = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
-            call("tmr_split_xpack", ptr(x), S, C, H, W, ks, PREC_CODES[prec], ptr(xmax), mode, ptr(out), stream())
+            call("tmr_split_xpack", ptr(x), S, C, H, W, 0, ks, PREC_CODES[prec], ptr(xmax), mode, ptr(out),
+                 stream())
             ref = _xrecords_ref(x, ks, prec, xmax.cpu().numpy() if mode else float(xmax.item()))
             got = out.view(torch.int16)
             assert got.numel() == ref.numel(), prec
@@ -344,7 +346,7 @@ def test_xpack_records_bitexact(S, C, H, W, ks):
             assert bad == 0, f"{prec}: {bad} of {ref.numel()} 16-bit words differ"
             if prec == "bf16" and W % 8 == 0:
                 # the bf16 input form (tmr_split_xpack16 of bf16(x), the bf16
-                # f_TM plane of tmr_xcorr_out): the same records bit for bit
+                # f_TM plane of tmr_xcorr out_bf16): the same records bit for bit
                 out16 = torch.full((n,), 0x5A, device="cuda", dtype=torch.uint8)
                 xb = x.to(torch.bfloat16)
                 call("tmr_split_xpack16", ptr(xb), S, C, H, W, ks, PREC_CODES[prec], ptr(out16), stream())
@@ -359,7 +361,7 @@ def test_split_acc_slab_bf16():
     contract; the flags are refused under the fp32 3-term split and without a
     tiled buffer."""
     from tmr_amd._lib import (PREC_CODES, SPLIT_INIT_BF16, SPLIT_OUT_BF16, SPLIT_TILED_INIT,
-                              SPLIT_TILED_OUT, call, load, ptr, stream)
+                              SPLIT_TILED_OUT, call, ptr, size, stream)
     from tmr_amd.engine import absmax, pack_split_w, pack_split_x
     torch.manual_seed(5)
     B, U, C0, C1, N, H, W = 2, 3, 40, 48, 136, 19, 37
@@ -384,13 +386,13 @@ def test_split_acc_slab_bf16():
     xp0, xp1 = pack_split_x(d["x0"], 3, "bf16", xm0), pack_split_x(d["x1"], 3, "bf16", xm1)
     slabs = {}
     for tag, fl in (("fp32", 0), ("bf16", SPLIT_OUT_BF16)):
-        slabs[tag] = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=DEV)
-        call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0),
-             ptr(xm0), ptr(zero), N, 0, None, ptr(slabs[tag]), SPLIT_TILED_OUT | fl, stream())
+        slabs[tag] = torch.empty(size("acc", B, N, H, W), device=DEV)
+        call("tmr_split_conv", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0),
+             ptr(xm0), ptr(zero), N, 0, None, None, ptr(slabs[tag]), SPLIT_TILED_OUT | fl, stream())
     got = {}
     for tag, fl in (("fp32", 0), ("bf16", SPLIT_INIT_BF16)):
-        part = torch.empty(load().tmr_heads_partials_size(N, U, H, W), device=DEV)
-        call("tmr_split_conv_heads", None, 0, ptr(uid), ptr(xp1), C1, U, H, W, 3, pc, ptr(wp1), ptr(wm1),
+        part = torch.empty(size("heads_partials", N, U, H, W), device=DEV)
+        call("tmr_split_conv", None, 0, ptr(uid), ptr(xp1), C1, U, H, W, 3, pc, ptr(wp1), ptr(wm1),
              ptr(xm1), ptr(d["b"]), N, 1, ptr(d["hw"]), ptr(slabs[tag]), ptr(part), SPLIT_TILED_INIT | fl,
              stream())
         o, bb = torch.empty((U, 1, H, W), device=DEV), torch.empty((U, 4, H, W), device=DEV)
@@ -402,15 +404,15 @@ def test_split_acc_slab_bf16():
     e_ref = max(normwise(got["bf16"][u], ref[u]) for u in range(U))
     print(f"bf16 slab vs fp32 slab {e_slab:.2e}, vs fp64 reference {e_ref:.2e}")
     assert 0.0 < e_slab <= 1e-2 and e_ref <= SPLIT_TOL["bf16"]
-    out = torch.empty(load().tmr_split_acc_size(B, N, H, W), device=DEV)
+    out = torch.empty(size("acc", B, N, H, W), device=DEV)
     wpf, wmf = pack_split_w(d["w0"], C0, "fp32")
     with pytest.raises(tmr_amd.TMRError):  # bf16 slabs are a one-term-precision layout
-        call("tmr_split_conv_store", ptr(pack_split_x(d["x0"], 3, "fp32", xm0)), C0, None, None, 0, B, H, W, 3,
-             PREC_CODES["fp32"], ptr(wpf), ptr(wmf), ptr(xm0), ptr(zero), N, 0, None, ptr(out),
+        call("tmr_split_conv", ptr(pack_split_x(d["x0"], 3, "fp32", xm0)), C0, None, None, 0, B, H, W, 3,
+             PREC_CODES["fp32"], ptr(wpf), ptr(wmf), ptr(xm0), ptr(zero), N, 0, None, None, ptr(out),
              SPLIT_TILED_OUT | SPLIT_OUT_BF16, stream())
     with pytest.raises(tmr_amd.TMRError):  # OUT_BF16 needs the tiled output
-        call("tmr_split_conv_store", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0), ptr(xm0),
-             ptr(zero), N, 0, None, ptr(out), SPLIT_OUT_BF16, stream())
+        call("tmr_split_conv", ptr(xp0), C0, None, None, 0, B, H, W, 3, pc, ptr(wp0), ptr(wm0), ptr(xm0),
+             ptr(zero), N, 0, None, None, ptr(out), SPLIT_OUT_BF16, stream())
 
 
 def test_shared_and_unshared_fp_half_agree():
@@ -1073,12 +1075,16 @@ def test_reduced_precision_forward_vs_oracle(prec):
 
 # ----------------------------------------------------------------- xcorr (MFMA)
 @pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15), (70, 128, 8, 31),
-                                        (192, 192, 8, 31), (33, 32, 8, 15)])
+                                        (192, 192, 8, 31), (33, 32, 8, 15), (128, 128, 8, 15),
+                                        (100, 192, 8, 21), (77, 128, 8, 9)])
 def test_xcorr_mfma_vs_oracle(H, W, C, kmax):
     """The row-Toeplitz MFMA correlation kernel (TMR_XCORR_MFMA, 3-term fp16
     split) against the C oracle at every odd template side 1..31, rectangular
-    templates, several units per image, band edges (H % 32 != 0), a learned
-    scale, relu output, the fused max |f_TM| and the zero pad border."""
+    templates, several units per image, band edges (H % 32 / % 64 != 0), a
+    learned scale, relu output, the fused max |f_TM| and the zero pad border.
+    Both band heights run: 64-row bands where the band and halo fit the
+    staging registers and a row is 8 or 12 tiles (W 128 / 192, kmax <= 21 at
+    192), 32-row bands otherwise (W 96 / 32, kmax 31 at 192)."""
     _xcorr_mfma_case(H, W, C, kmax, "fp32")
 
 
@@ -1090,16 +1096,17 @@ XCORR_ONE_TERM_TOL = {"bf16": 1e-2, "f16": 2e-3}
 
 
 @pytest.mark.parametrize("prec", ["bf16", "f16"])
-@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15)])
+@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15), (128, 128, 8, 15),
+                                        (100, 192, 8, 21)])
 def test_xcorr_mfma_one_term_vs_oracle(H, W, C, kmax, prec):
-    """tmr_xcorr_prec with one bf16 / fp16 MFMA term: the same shapes, border,
+    """tmr_xcorr with one bf16 / fp16 MFMA term: the same shapes, border,
     relu and fused-max contract as the 3-term kernel, at the one-term tolerance;
     the VALU kernel in the same call stays fp32 (1e-5)."""
     _xcorr_mfma_case(H, W, C, kmax, prec)
 
 
 def _xcorr_mfma_case(H, W, C, kmax, prec):
-    from tmr_amd._lib import PREC_CODES, XCORR_ALGOS, call, ptr, stream
+    from tmr_amd._lib import PREC_CODES, XCORR_ALGOS, call, ptr, size, stream, xcorr
     from tmr_amd.engine import _h2d, _units_to_device
     B = 2
     f = synth.normal(90 + H + W, (B, C, H, W)) * 1.7
@@ -1120,18 +1127,19 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
     iu = _h2d(host.image_ranges(ui, B), DEV)
     U = len(ui)
     scale = torch.tensor([0.75], device=DEV)
-    lib = tmr_amd._lib.load()
     rows = host.tsplit_rows(units)
-    tsplit = torch.empty(lib.tmr_template_split_size(U, C, rows), device=DEV, dtype=torch.uint8)
+    tsplit = torch.empty(size("template_split", U, C, rows), device=DEV, dtype=torch.uint8)
     pc = PREC_CODES[prec]
-    call("tmr_template_split_prec", ptr(tmpl), ptr(ud), U, C, rows, pc, ptr(tsplit), stream())
+    call("tmr_template_split", ptr(tmpl), ptr(ud), U, C, rows, pc, ptr(tsplit), stream())
+    common = dict(f=ptr(fd), templates=ptr(tmpl), units=ptr(ud), img_units=ptr(iu), scale=ptr(scale),
+                  tmpl_split=ptr(tsplit), total_rows=rows, B=B, C=C, H=H, W=W, U=U, max_ht=mh, max_wt=mw,
+                  min_k=1, stream=stream())
     outs = {}
     for algo in ("valu", "mfma"):
         out = torch.empty((U, C, H, W), device=DEV)
         relu = torch.empty_like(out)
         amax = torch.zeros(U, device=DEV)
-        call("tmr_xcorr_prec", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
-             ptr(out), ptr(relu), None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, stream())
+        xcorr(out=ptr(out), relu_out=ptr(relu), out_absmax=ptr(amax), algo=XCORR_ALGOS[algo], prec=pc, **common)
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         outs[algo] = got
@@ -1139,19 +1147,24 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
         assert np.array_equal(amax.cpu().numpy(), np.abs(got).reshape(U, -1).max(1)), algo
         assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0)), algo
         if algo == "mfma" and prec == "bf16":
-            # tmr_xcorr_out's bf16 plane: RNE bf16 of the fp32 plane, bit for bit
+            # tmr_xcorr's bf16 plane (out_bf16): RNE bf16 of the fp32 plane, bit for bit
             o16 = torch.empty((U, C, H, W), device=DEV, dtype=torch.bfloat16)
-            call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw, ptr(scale), 0,
-                 ptr(o16), None, None, ptr(amax), ptr(tsplit), rows, XCORR_ALGOS[algo], 1, pc, 1, stream())
+            xcorr(out=ptr(o16), out_absmax=ptr(amax), algo=XCORR_ALGOS[algo], prec=pc, out_bf16=1, **common)
             torch.cuda.synchronize()
             assert torch.equal(o16.view(torch.int16), out.to(torch.bfloat16).view(torch.int16))
             # refused with a relu output, on the VALU kernel and on other precisions
             for bad in ((ptr(relu), XCORR_ALGOS["mfma"], pc), (None, XCORR_ALGOS["valu"], pc),
                         (None, XCORR_ALGOS["mfma"], PREC_CODES["f16"])):
                 with pytest.raises(tmr_amd.TMRError):
-                    call("tmr_xcorr_out", ptr(fd), B, C, H, W, ptr(tmpl), ptr(ud), ptr(iu), U, mh, mw,
-                         ptr(scale), 0, ptr(o16), bad[0], None, None, ptr(tsplit), rows, bad[1], 1, bad[2], 1,
-                         stream())
+                    xcorr(out=ptr(o16), relu_out=bad[0], algo=bad[1], prec=bad[2], out_bf16=1, **common)
+            # AUTO without the split templates runs the VALU kernel (no MFMA operands): the fp32 plane
+            o_auto = torch.empty((U, C, H, W), device=DEV)
+            cm = dict(common, tmpl_split=None, total_rows=0)
+            xcorr(out=ptr(o_auto), algo=XCORR_ALGOS["auto"], prec=pc, **cm)
+            torch.cuda.synchronize()
+            assert normwise(o_auto.cpu().numpy(), outs["valu"]) == 0.0
+            with pytest.raises(tmr_amd.TMRError):  # MFMA without them is unsupported
+                xcorr(out=ptr(o_auto), algo=XCORR_ALGOS["mfma"], prec=pc, **cm)
     tol = {"valu": TOL, "mfma": TOL if prec == "fp32" else XCORR_ONE_TERM_TOL[prec]}
     tmpl_h = tmpl.cpu().numpy()
     worst = 0.0
@@ -1174,12 +1187,10 @@ def _xcorr_mfma_case(H, W, C, kmax, prec):
 
 def test_engine_bf16_ftm_plane_bitexact():
     """Under the bf16 contract the detect path's correlation writes f_TM as
-    bf16 (tmr_xcorr_out) -- as a plane the decoder packs with
-    tmr_split_xpack16, or as the decoder's records themselves (the record
-    mode, the ring zeroed by tmr_split_xpack_ring): the maps are
-    bit-identical to the fp32-plane path (engine.out_bf16 = False), for the
-    shared (E = 3) and the unshared (E = 1) fp half, decoder kernel sizes 3
-    and 5."""
+    bf16 (tmr_xcorr out_bf16), a plane the decoder packs with
+    tmr_split_xpack16: the maps are bit-identical to the fp32-plane path
+    (engine.out_bf16 = False), for the shared (E = 3) and the unshared (E = 1)
+    fp half, decoder kernel sizes 3 and 5."""
     cin, emb, hf = 64, 128, 32
     for k in (3, 5):
         P = synth.reference_state_dict(9, cin=cin, emb=emb, obj_bias=-0.3, k=k)
@@ -1188,18 +1199,16 @@ def test_engine_bf16_ftm_plane_bitexact():
             ex, _ = synth.exemplar_set(71 + E, B, E, 2 * hf, 2 * hf, 3, 15)
             ui = np.repeat(np.arange(B), E)
             res = {}
-            for mode in ("fp32", "plane", "records"):
+            for mode in ("fp32", "plane"):
                 eng = tmr_amd.TMREngine({k_: cuda(v) for k_, v in P.items()},
                                         tmr_amd.PathConfig(emb_dim=emb, precision="bf16", decoder_kernel_size=k))
                 eng.xcorr_algo = "mfma"
                 eng.out_bf16 = mode != "fp32"
-                eng.out_records = mode == "records"
                 r = eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4))
                 assert eng.last_xcorr_out16 == (mode != "fp32")
                 res[mode] = (r["o"].cpu().numpy(), r["b"].cpu().numpy())
-            for mode in ("plane", "records"):
-                for a, b in zip(res["fp32"], res[mode]):
-                    assert bits_equal(a, b), (k, B, E, mode)
+            for a, b in zip(res["fp32"], res["plane"]):
+                assert bits_equal(a, b), (k, B, E)
         # the module form (relu(f_TM) returned) keeps the fp32 plane
         eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
         assert not eng.last_xcorr_out16
@@ -1226,68 +1235,6 @@ def test_xcorr_mfma_squeeze_and_engine():
             ref = oracle.xcorr(f[ui[u]], t, 1.25, sq)
             for algo in ("valu", "mfma", "auto"):
                 assert normwise(res[(sq, algo)][u], ref) <= TOL, (sq, algo, u)
-
-
-def test_xcorr_split_launch_matches_single_kernel_launches():
-    """TMREngine.xcorr_split: a mixed launch split per unit by the cost model
-    into a VALU launch (side stream) and an MFMA launch (current stream) over
-    complementary unit subsets (tmr_unit_t.out_unit): every unit's f_TM and
-    relu(f_TM), and its fused max |f_TM|, are bit-identical to the
-    single-kernel launch of its own kernel over the whole batch."""
-    from tmr_amd.engine import xcorr_unit_split
-    C, H, W, B, E = 32, 128, 128, 4, 3
-    P = {k: cuda(v) for k, v in synth.reference_state_dict(31, cin=16, emb=C).items()}
-    fp = cuda(synth.normal(32, (B, C, H, W)))
-    ex, ks = synth.exemplar_set(33, B, E, H, W, 3, 15)
-    boxes, ui = ex.reshape(-1, 4), np.repeat(np.arange(B), E)
-    res = {}
-    for mode in ("valu", "mfma", "split"):
-        eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C))
-        eng.xcorr_algo = "auto" if mode == "split" else mode
-        eng.xcorr_split = mode == "split"
-        if mode == "split":  # force a mixed set whatever the cost table says
-            import tmr_amd.engine as E_
-            orig = E_.xcorr_unit_split
-            E_.xcorr_unit_split = lambda ht, wt, upi, one_term=False: np.maximum(ht, wt) >= 11
-        try:
-            f, relu = eng.match(fp, ui, boxes, want_relu=True)
-        finally:
-            if mode == "split":
-                E_.xcorr_unit_split = orig
-        torch.cuda.synchronize()
-        res[mode] = (f.cpu().numpy(), relu.cpu().numpy(), eng._memo_absmax(f, "ftm").cpu().numpy(),
-                     eng.last_xcorr_algo)
-    assert res["split"][3] == "split"
-    for u in range(B * E):
-        k = max(host.template_size(boxes[u], H, W)[1:])
-        src = "mfma" if k >= 11 else "valu"
-        for t in range(3):
-            assert bits_equal(res["split"][t][u], res[src][t][u]), (u, k, t)
-    assert xcorr_unit_split(np.array([3, 15]), np.array([3, 15]), 3.0).tolist() == [False, True]
-
-
-@pytest.mark.parametrize("prec", ["fp32", "bf16", "f16"])
-@pytest.mark.parametrize("H,W,kmax", [(128, 128, 15), (96, 192, 31)])
-def test_xcorr_mfma_lds_fragments_bitexact(prec, H, W, kmax):
-    """The MFMA correlation with its A fragments built in-kernel from the
-    LDS-staged template (tmpl_split NULL, TMREngine.xcorr_afrag "lds") gives
-    the same f_TM, relu(f_TM) and per-unit max bit for bit as with the
-    pre-expanded fragments of tmr_template_split (3-term split; the one-term
-    precisions keep the pre-expanded fragments, so "lds" changes nothing)."""
-    C, B, E = 24, 2, 5
-    P = {k: cuda(v) for k, v in synth.reference_state_dict(41, cin=16, emb=C).items()}
-    fp = cuda(synth.normal(42 + W, (B, C, H, W)))
-    ex, _ = synth.exemplar_set(43 + kmax, B, E, H, W, 1, kmax)
-    boxes, ui = ex.reshape(-1, 4), np.repeat(np.arange(B), E)
-    res = {}
-    for af in ("split", "lds"):
-        eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C, precision=prec))
-        eng.xcorr_algo, eng.xcorr_afrag = "mfma", af
-        f, relu = eng.match(fp, ui, boxes, want_relu=True)
-        torch.cuda.synchronize()
-        res[af] = (f.float().cpu().numpy(), relu.float().cpu().numpy(), eng._memo_absmax(f, "ftm").cpu().numpy())
-    for t in range(3):
-        assert bits_equal(res["lds"][t], res["split"][t]), (prec, t)
 
 
 @pytest.mark.parametrize("thr", [0.1, 0.5, 0.999, 0.9999999, 0.99999994, 1.0, 0.0, 1e-30])
