@@ -122,8 +122,9 @@ int tmr_templates(const float *f, int B, int C, int H, int W, const tmr_unit_t *
  *  max |out[u]| per unit (the split decoder's per-unit activation scale
  *  source, TMR_SPLIT_XMAX_PER_UNIT), with no extra pass over out.
  *  algo: TMR_XCORR_VALU (fp32 LDS-blocked wavefront kernels), TMR_XCORR_MFMA
- *  (row-Toeplitz implicit GEMM on v_mfma_f32_16x16x32_{f16,bf16}: W % 32 == 0,
- *  W <= 256, templates <= 31x31, tmpl_split given; TMR_E_UNSUPPORTED
+ *  (2-D window Toeplitz implicit GEMM on v_mfma_f32_16x16x32_{f16,bf16}:
+ *  W % 64 == 0, W <= 256, templates <= 31x31, the staged band fits,
+ *  tmpl_split given; TMR_E_UNSUPPORTED
  *  otherwise) or TMR_XCORR_AUTO (MFMA when it fits, tmpl_split is given and
  *  min_k -- the smallest template side of the launch -- reaches the
  *  crossover; VALU otherwise).

@@ -496,41 +496,60 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
 
 // ---------------------------------------------------------------------------
 // MFMA variant (kernel (2) of BASELINE north_star): the depthwise correlation
-// as a row-Toeplitz GEMM on v_mfma_f32_16x16x32_f16 with an fp32-grade
+// as a 2-D Toeplitz GEMM on v_mfma_f32_16x16x32_{f16,bf16} with an fp32-grade
 // 3-term split (the decoder's F16X3 scheme, conv_split.hip).
 //
-// For channel c, template row i and a 16x16 output tile at (y0, x0):
-//   D[m][n] = sum_k A_i[m][k] B_i[k][n],  m = output col x0+m, n = output row
-//   y0+n, k = input col a0+k (a0 = x0 - pw_al, pw_al = 8*ceil(pw/8)),
-//   A_i[m][k] = T[i][k - m - s]  (s = pw_al - pw; zero outside [0, w)),
-//   B_i[k][n] = F[y0 + n - ph + i][a0 + k],
-// summed over i = 0..h-1 (the template rows) into one accumulator; K per row
-// is 32 * NK with NK = ceil((16 + s + w - 1) / 32) (1 for w <= 17, 2 to 31).
+// Geometry (round 6).  M = 16 outputs of one PATCH, 2 output rows x 8 output
+// columns (r, c); K = 32 inputs of one WINDOW, 4 input rows x 8 input columns
+// (iy, ix); N = 16 patches.  For a patch at (y0, x0) and window (a, b):
+//   A_ab[(r,c)][(iy,ix)] = T[4a + iy - r][8b + ix - c - s],  zero outside the template,
+//   B_ab[(iy,ix)][n]     = F[y0(n) - ph + 4a + iy][x0(n) - pw - s + 8b + ix],
+// summed over the windows a < ceil((h+1)/4), b < ceil((w+7+s)/8), where
+// s = (-pw) mod 8 aligns every window's first column to 8 fp16 (16 bytes:
+// each B chunk is one ds_read_b128).  A depends on the template and (a, b)
+// only -- one pre-expanded 1-KB fragment per window and term
+// (tmr_template_split), shared by every patch.  The K window is dense in the
+// template's interior, so the useful share of each MFMA is
+// h*w / (32 * windows): at k = 9 / 15 / 19 / 31, 0.28 / 0.59 / 0.45 / 0.75,
+// against 0.28 / 0.47 / 0.30 / 0.48 of the round-5 row Toeplitz (one template
+// row x 32 input columns per MFMA, 16 outputs of one row): the config-B mix
+// (k 3..15) runs 10% fewer MFMAs, the config-E mix (k 3..31) 29% fewer.  The
+// MFMA shape study (profiles/mfma_shapes, round 6: random operands, every
+// 16-bit gfx950 form) found no shape with a better useful rate -- 16x16x16 /
+// 32x32x8 run at 0.65 of 16x16x32's FLOP rate, the 4x4x4 and 16x16x4
+// multi-block forms at 0.31 / 0.36 -- so the geometry, not the instruction,
+// changed.
+//
+// The 16 patches of one accumulator tile 4 output rows x 64 columns: patch n
+// at (R + 2 (n >> 3), C0 + 8 (n & 7)).  Lane (n, g) of D holds output row
+// R + 2 (n >> 3) + (g >> 1), columns C0 + 8 (n & 7) + 4 (g & 1) + 0..3: one
+// 16-B store, 256 contiguous bytes per row per wave instruction.
+//
 // Both operands are split x*s_x = xh + xl (fp16, power-of-two scales: the
 // staged band's max for F, the template's max for T) and every product is
 // th*fh + th*fl + tl*fh with fp32 accumulation (dropped tl*fl and the split
 // residuals ~2^-22 relative), then exactly unscaled, divided by fl32(h*w)
 // correctly rounded and scaled like the VALU kernels.
 //
-// Block = (band of 32 output rows, channel, image), 4 waves; the band's input
-// rows (+- the largest template's half height, zero rows outside the image,
-// zero columns left/right) are staged ONCE as fp16 hi/lo planes and reused
-// by every exemplar unit of the image.  Wave w owns tile row (w & 1) and every
-// other 16-col tile: its A (template) fragments are built once per template
-// row and reused across its NTW tiles.  LDS row stride SB = 32 mod 64 bytes
-// makes the B-fragment reads (16 lanes = 16 rows, same column) conflict free
-// for all four ds_read_b128 lane groups.  The 1-D grid is remapped so each
-// XCD runs a contiguous range of (band, channel, image) blocks: neighbouring
-// bands' halo rows meet in that XCD's L2.
-constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw_al)
-// A-fragment prefetch distance in template rows.  One-term kernel: 4 rows
-// (its rows are 1/3 the MFMA work of the 3-term kernel's, so one row ahead
-// leaves the L2 latency exposed; measured at 128^2 E = 3, config-B mix: PF
-// 1/2/3/4/5/8 = 3.74/4.10/3.61/3.09/4.56/3.24 ms, profiles/archive/r02ad_*, r02ae_*).
-// 3-term kernel: 1 row (PF 2/4: 5.85/5.28 vs 4.67 ms).
-// 3-term, >= 6 tiles per wave (W >= 192, LDS-bound occupancy): 3 rows (r03t).
-constexpr int XCORR_PF1 = 4, XCORR_PF3 = 1, XCORR_PF3_WIDE = 3;
+// Block = (band of BR output rows, channel, image), 4 waves; the band's input
+// rows (+- the image's largest template half height, zero rows outside the
+// image, zero columns left/right) are staged ONCE as fp16 hi/lo planes and
+// reused by every exemplar unit of the image.  Wave w owns BR/16 row quads of
+// the band, every 64-column group of them.  LDS rows: see band_stride (B
+// reads conflict free).  The 1-D grid is remapped so each XCD runs a
+// contiguous range of (band, channel, image) blocks: neighbouring bands' halo
+// rows meet in that XCD's L2.
+constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw + s = 16 at most)
+constexpr int MPADR = 24;   // zero fp16 columns right of the image (>= pw + 7)
+// A-fragment prefetch distance in windows: the 3-term kernel's windows are
+// 3 MFMAs per accumulator, the one-term kernel's 1
+constexpr int XCORR_PF3 = 2, XCORR_PF1 = 4;
 constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
+// The last window row block of a template reaches up to 3 rows past the
+// h + 1 input rows of a 2-row patch (4 ceil((h + 1) / 4) >= h + 1); its A
+// taps there are zero, but zero x (stale LDS bits) can be NaN, so the band
+// stages WIN_OVER more (zero) rows below the halo.
+constexpr int WIN_OVER = 3;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -562,9 +581,10 @@ __device__ __forceinline__ f32x4 xmma(b8 a, b8 b, f32x4 c) {
 }
 
 struct MArgs {
-    int SB;     // LDS plane row stride in bytes (32 mod 64)
-    int LR;     // staged rows: band rows + 2 * HG
+    int SB;     // LDS plane row stride in bytes (128 mod 256)
+    int LR;     // staged rows: band rows + 2 * HG + WIN_OVER
     int HG;     // max template height / 2
+    int BR;     // output rows per block (64 or 32)
     int nband;  // bands per channel plane
     int nlog;   // logical blocks = nband * C * B
 };
@@ -591,29 +611,23 @@ __device__ __forceinline__ float block_max(float v, float *red) {
 // Per (unit, channel) split of the exemplar templates for the MFMA kernel
 // (tmr_template_split): t * 2^-et = th + tl (fp16) with 2^-et the power-of-two
 // scale of the template's own max |t| (max |t| 2^-et < 2^14), written as the
-// kernel's A fragments themselves: for template row i, K block nk and term
-// (hi, lo), 64 lanes x 16 B in lane order, lane (m, g) holding the taps
-// T[i][8g + 32nk + q - m - s], q = 0..7 (zero outside [0, w)).  The kernel's
-// A load is then one aligned, contiguous 1-KB wave read.  (Loading the same
-// 16-B windows at 2-B-aligned offsets out of padded template rows -- round 2's
-// first layout -- cost 17-21% of the kernel at k = 15: profiles/archive/r02u_*.)
-// One wave per (unit, channel).
-constexpr int AFRAG = 64 * 16;  // bytes per (row, nk, term) fragment
+// kernel's A fragments themselves: for window (a, b) and term (hi, lo), 64
+// lanes x 16 B in lane order, lane (m, g) holding T[4a + g - (m >> 3)]
+// [8b + q - (m & 7) - s], q = 0..7 (zero outside the template).  The
+// kernel's A load is one aligned, contiguous 1-KB wave read per window and
+// term.  One wave per (unit, channel).
+constexpr int AFRAG = 64 * 16;  // bytes per (window, term) fragment
 
 // Template split of the 3-term fragments: t 2^-e = th + tl with th rounded to
 // TH_BITS significant bits (exact in fp16) and tl = fp16(t 2^-e - th), the
-// correlation's counterpart of conv_split.hip's WH_BITS (th feeds two of the
-// three MFMAs per product; fewer set bits, less MFMA power).  11 = the plain
-// fp16 hi/lo split, kept: unlike the decoder (busy 0.83, power-bound) this
-// kernel gains nothing measurable (profiles/r04k, A/B in one call: config-E
-// mix 12.21 / 12.19 -> 12.14 / 12.12 ms at 6 bits, config-B mix 4.49 / 4.51
-// -> 4.47 / 4.51) for a 2-5x larger error (4e-7..1.5e-6 -> 1.1e-6..2.3e-6).
+// correlation's counterpart of conv_split.hip's WH_BITS.  11 = the plain fp16
+// hi/lo split (profiles/r04k: fewer hi bits measured no faster here).
 constexpr int TH_BITS = 11;
 
-__host__ __device__ inline int tsplit_nk(int w) {  // K blocks of 32 per template row
-    const int pw = w / 2, s = ((pw + 7) & ~7) - pw;
-    return 16 + s + w - 1 <= 32 ? 1 : 2;
-}
+__host__ __device__ inline int win_s(int w) { return (8 - ((w / 2) & 7)) & 7; }  // (-pw) mod 8
+__host__ __device__ inline int win_na(int h) { return (h + 4) / 4; }                  // ceil((h + 1) / 4)
+__host__ __device__ inline int win_nb(int w) { return (w + win_s(w) + 14) / 8; }     // ceil((w + 7 + s) / 8)
+__host__ __device__ inline int win_count(int h, int w) { return win_na(h) * win_nb(w); }
 
 __global__ __launch_bounds__(256) void template_split_kernel(const float *__restrict__ tmpl,
                                                              const tmr_unit_t *__restrict__ units, int U,
@@ -621,8 +635,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                                                              char *__restrict__ frags,
                                                              int32_t *__restrict__ exps) {
     // the wave's template through LDS (coalesced global reads once; the
-    // fragments' lane-shifted taps are then LDS reads, not 8 scattered global
-    // loads per lane and fragment)
+    // fragments' lane-shifted taps are then LDS reads)
     __shared__ float tsh[4][31 * 31];
     const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
@@ -646,18 +659,19 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     int et;
     const float st = pow2_scale(m, et);
-    const int nk_u = tsplit_nk(w), pw = w / 2, s = ((pw + 7) & ~7) - pw;
-    const int mm = lane & 15, g = lane >> 4;
-    char *dst = frags + ((int64_t)C * un.row_offset + (int64_t)c * h * nk_u) * 2 * AFRAG + lane * 16;
-    for (int i = 0; i < h; ++i)
-        for (int nk = 0; nk < nk_u; ++nk) {
+    const int na = win_na(h), nb = win_nb(w), s = win_s(w);
+    const int mm = lane & 15, g = lane >> 4, r = mm >> 3, cc = mm & 7;
+    char *dst = frags + ((int64_t)C * un.row_offset + (int64_t)c * na * nb) * 2 * AFRAG + lane * 16;
+    for (int a = 0; a < na; ++a) {
+        const int i = 4 * a + g - r;
+        for (int b = 0; b < nb; ++b) {
             float x[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int j = 8 * g + 32 * nk + q - mm - s;
-                x[q] = (j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
+                const int j = 8 * b + q - cc - s;
+                x[q] = (i >= 0 && i < h && j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
             }
-            char *f = dst + (size_t)((i * nk_u + nk) * 2) * AFRAG;
+            char *f = dst + (size_t)((a * nb + b) * 2) * AFRAG;
             if (bf) {  // wave-uniform: bf16 hi (the one-term bf16 MFMA reads hi only)
                 b8 hi;
 #pragma unroll
@@ -675,68 +689,99 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 if (lo_too) *reinterpret_cast<h8 *>(f + AFRAG) = lo;  // the 3-term kernel's tl
             }
         }
+    }
     if (lane == 0) exps[(int64_t)u * C + c] = et;
 }
 
-// one unit over the band: acc[t] += sum_i A_i B_i over the wave's NTW tiles
-// (tile cols tcol0 + WPR t).  The A fragments -- lane (m, g): taps
-// T[i][8g + 32nk + q - m - s], q = 0..7 -- are aligned 16-B lane loads of the
-// pre-expanded fragments (tmr_template_split; arow = this lane's slot of
-// row 0), issued PF template rows ahead of their MFMAs.  (Measured: staging
-// them through an LDS table per row chunk, with its two barriers per chunk,
-// was slower at every k >= 11; profiles/archive/r02b_kbench_xcorr_*.)
-template <int NTW, int NK, int WPR, int PM>
-__device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, const char *Fl, int SB, int rb,
-                                          int h, const char *arow, int tcol0, int pw_al, int g) {
+// LDS row stride of a band W = 64 NCG columns wide (MPADL + W + MPADR fp16
+// per row): the smallest stride >= the row that is 128 or 0 mod 256 bytes.
+// The 16 lanes of a ds_read_b128 group read 16 B each from 4 rows (2 patch
+// rows x 2 window rows), 4 lanes per row over 64 contiguous bytes; the rows
+// fall on disjoint banks when odd rows sit 128 mod 256 bytes from even ones:
+// by the stride itself (128 mod 256), or (0 mod 256) by XOR-ing bit 7 of the
+// byte column of odd rows.  W 64 / 128 / 192 / 256: 256 (XOR) / 384 / 512
+// (XOR) / 640 B.
+__host__ __device__ constexpr int band_stride(int ncg) {
+    const int bytes = 2 * (64 * ncg + MPADL + MPADR);
+    const int a = (bytes + 127) / 256 * 256 + 128, b = (bytes + 255) / 256 * 256;
+    return a < b ? a : b;
+}
+// XOR applied to the byte column of staged row lr: bit 7 of odd rows under a
+// 0 mod 256 stride (the same for rows 4 apart: windows and row quads)
+template <int SB>
+__device__ __forceinline__ int band_swz(int lr) {
+    if constexpr (SB % 256 == 0) return (lr & 1) ? 128 : 0;
+    else return 0;
+}
+template <int SB>
+__device__ __forceinline__ int lds_off(int lr, int col) {  // col % 4 == 0 (elements)
+    return lr * SB + ((2 * col) ^ band_swz<SB>(lr));
+}
+
+// One unit over the wave's accumulators: acc[t] += sum over windows of
+// A_ab B_ab(t).  Accumulator t = (row quad tq, 64-column group tc).  `rh` /
+// `rl`: the hi / lo plane's staged row of this lane's B chunk at window row
+// block a = 0, accumulator row quad 0; `cb`: the chunk's logical byte column
+// at b = 0, accumulator column group 0 (16-B aligned); `swz`: the row's
+// swizzle (rows move by 4 per window row block and row quad, so it is the
+// same for all).  Each window's B chunks of every accumulator are loaded
+// first (one ds_read_b128 per plane and accumulator, logical column
+// cb + 16 b + 128 tc), then its MFMAs; the A fragments (hi and lo) are
+// aligned 16-B lane loads of the pre-expanded fragments, issued PF windows
+// ahead.
+template <int NRQ, int NCG, int PM>
+__device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NRQ * NCG], const char *rh, const char *rl, int cb, int swz,
+                                          int na, int nb, const char *arow) {
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int PF = SPLIT ? (NTW >= 6 ? XCORR_PF3_WIDE : XCORR_PF3) : XCORR_PF1;  // (rows)
-    V ah[PF][NK], al[PF][NK];
-    auto afrag = [&](int i, int nk, int term) -> V {
-        return *reinterpret_cast<const V *>(arow + (size_t)((i * NK + nk) * 2 + term) * AFRAG);
+    constexpr int PF = SPLIT ? XCORR_PF3 : XCORR_PF1;  // (windows)
+    constexpr int SB = band_stride(NCG);
+    constexpr int NACC = NRQ * NCG;
+    const int nw = na * nb;
+    V ah[PF], al[PF];
+    auto afrag = [&](int wi, int term) -> V {
+        return *reinterpret_cast<const V *>(arow + (size_t)(wi * 2 + term) * AFRAG);
     };
 #pragma unroll
     for (int p = 0; p < PF; ++p)
-        if (p < h) {
-#pragma unroll
-            for (int nk = 0; nk < NK; ++nk) {
-                ah[p][nk] = afrag(p, nk, 0);
-                if (SPLIT) al[p][nk] = afrag(p, nk, 1);
-            }
+        if (p < nw) {
+            ah[p] = afrag(p, 0);
+            if (SPLIT) al[p] = afrag(p, 1);
         }
-    for (int i0 = 0; i0 < h; i0 += PF) {
+    int a = 0, b = 0;
+    for (int w0 = 0; w0 < nw; w0 += PF) {
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
-            const int i = i0 + p;
-            if (i >= h) break;
-            const char *rh = Fh + (size_t)(rb + i) * SB, *rl = Fl + (size_t)(rb + i) * SB;
-            V ch[NK], cl[NK];
+            const int wi = w0 + p;
+            if (wi >= nw) break;
+            const int ro = a * 4 * SB, cw = cb + 16 * b;
+            V xb[NACC], xl[NACC];
 #pragma unroll
-            for (int nk = 0; nk < NK; ++nk) {
-                ch[nk] = ah[p][nk];
-                if (SPLIT) cl[nk] = al[p][nk];
-            }
-            if (i + PF < h) {
+            for (int tc = 0; tc < NCG; ++tc) {
+                const int c0 = ro + ((cw + 128 * tc) ^ swz);
 #pragma unroll
-                for (int nk = 0; nk < NK; ++nk) {
-                    ah[p][nk] = afrag(i + PF, nk, 0);
-                    if (SPLIT) al[p][nk] = afrag(i + PF, nk, 1);
+                for (int tq = 0; tq < NRQ; ++tq) {
+                    const int o = c0 + tq * 4 * SB;
+                    xb[tq * NCG + tc] = *reinterpret_cast<const V *>(rh + o);
+                    if (SPLIT) xl[tq * NCG + tc] = *reinterpret_cast<const V *>(rl + o);
                 }
             }
+            const V ch = ah[p];
+            V cl;
+            if (SPLIT) cl = al[p];
+            if (wi + PF < nw) {
+                ah[p] = afrag(wi + PF, 0);
+                if (SPLIT) al[p] = afrag(wi + PF, 1);
+            }
 #pragma unroll
-            for (int nk = 0; nk < NK; ++nk) {
-#pragma unroll
-                for (int t = 0; t < NTW; ++t) {
-                    const int colb = 2 * ((tcol0 + WPR * t) * 16 - pw_al + MPADL + 32 * nk + 8 * g);
-                    const V bh = *reinterpret_cast<const V *>(rh + colb);
-                    acc[t] = xmma(ch[nk], bh, acc[t]);
-                    if (SPLIT) {
-                        const V bl = *reinterpret_cast<const V *>(rl + colb);
-                        acc[t] = xmma(ch[nk], bl, acc[t]);
-                        acc[t] = xmma(cl[nk], bh, acc[t]);
-                    }
+            for (int t = 0; t < NACC; ++t) {
+                acc[t] = xmma(ch, xb[t], acc[t]);
+                if (SPLIT) {
+                    acc[t] = xmma(ch, xl[t], acc[t]);
+                    acc[t] = xmma(cl, xb[t], acc[t]);
                 }
             }
+            if (++b == nb) { b = 0; ++a; }
         }
     }
 }
@@ -744,7 +789,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NTW], const char *Fh, con
 // OB: f_TM leaves as bf16 (the bf16 contract's detect path: the decoder's
 // bf16 records are bf16(f_TM) either way, so the fp32 plane is never needed;
 // half the bytes written here and read by the record pack)
-template <int NTW, int NV4, int TRB, int PM, bool OB = false>
+template <int NRQ, int NCG, int NV4, int PM, bool OB = false>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
@@ -753,8 +798,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     typedef typename XOp<PM>::V4 V4;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
     constexpr int NPL = SPLIT ? 2 : 1;  // staged planes (hi, lo)
-    constexpr int WPR = 4 / TRB;  // waves per tile row
-    constexpr int BR = 16 * TRB;  // output rows per block
+    constexpr int NACC = NRQ * NCG;
+    constexpr int SB = band_stride(NCG);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // XCD-aware map: hardware block L runs on XCD L % 8; give each XCD a
     // contiguous range of logical blocks (band fastest)
@@ -762,7 +807,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     const int q = (L & 7) * per + (L >> 3);
     if (q >= m.nlog) return;
     const int band = q % m.nband, c = (q / m.nband) % a.C, img = q / (m.nband * a.C);
-    const int H = a.H, W = a.W, SB = m.SB, LR = m.LR, hg = m.HG;
+    const int H = a.H, W = a.W, LR = m.LR, hg = m.HG, BR = m.BR;
     const int u_beg = __builtin_amdgcn_readfirstlane(a.img_units[img]);
     const int u_end = __builtin_amdgcn_readfirstlane(a.img_units[img + 1]);
     if (u_beg >= u_end) return;
@@ -798,15 +843,16 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
             v[k] = reinterpret_cast<const float4 *>(fc + (size_t)yy * W)[cc];
         vm = fmaxf(vm, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
     }
-    // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both planes
+    // zero pad columns: [0, MPADL) and [MPADL + W, SB / 2) of every row, both
+    // planes, in 16-B pieces
     {
-        const int pr = SB / 16 - W / 8;   // 16-B pieces of pad per row (2 left, rest right)
+        const int pr = SB / 16 - W / 8;   // 16-B pieces of pad per row (MPADL / 8 left, the rest right)
         const float rpr = 1.0f / (float)pr;
         for (int e = tid; e < NPL * LR * pr; e += NT) {
             const int pl = SPLIT ? e & 1 : 0, rr = SPLIT ? e >> 1 : e;
             const int r = (int)(((float)rr + 0.5f) * rpr), j = rr - r * pr;
             const int col = j < MPADL / 8 ? 8 * j : W + 8 * j;
-            *reinterpret_cast<h8 *>((pl ? Fl : Fh) + (size_t)r * SB + 2 * col) = h8{};
+            *reinterpret_cast<h8 *>((pl ? Fl : Fh) + lds_off<SB>(r, col)) = h8{};
         }
     }
     int ef;
@@ -818,7 +864,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         const int lr = (int)(((float)e + 0.5f) * rw4), cc = e - lr * W4;
         const float x0 = v[k].x * sf, x1 = v[k].y * sf, x2 = v[k].z * sf, x3 = v[k].w * sf;
         const V4 hv = {(E)x0, (E)x1, (E)x2, (E)x3};
-        const size_t off = (size_t)lr * SB + 2 * (MPADL + 4 * cc);
+        const int off = lds_off<SB>(lr, MPADL + 4 * cc);
         *reinterpret_cast<V4 *>(Fh + off) = hv;
         if (SPLIT) {
             const V4 lv = {(E)(x0 - (float)hv[0]), (E)(x1 - (float)hv[1]), (E)(x2 - (float)hv[2]),
@@ -828,10 +874,9 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
     }
     __syncthreads();
 
-    const int lane = tid & 63, wave = tid >> 6, l16 = lane & 15, g = lane >> 4;
-    const int tr = wave % TRB;       // tile row of this wave
-    const int tcol0 = wave / TRB;    // tile cols tcol0, tcol0 + WPR, ...
-    const bool row_live = yb0 + tr * 16 < yb1;
+    const int lane = tid & 63, wave = tid >> 6, n = lane & 15, g = lane >> 4;
+    const int pr = n >> 3, pc = n & 7;
+    const int rq0 = wave * 4 * NRQ;  // the wave's first output row in the band (NRQ quads of 4 rows)
     const size_t plane = (size_t)H * W;
     for (int u = u_beg; u < u_end; ++u) {
         float vmax = 0.0f;
@@ -841,18 +886,18 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         const int roff = __builtin_amdgcn_readfirstlane(un.row_offset);
         const int et = __builtin_amdgcn_readfirstlane(texp[(size_t)uo * a.C + c]);
         const int ph = h / 2, pw = w / 2, Ho = H - h + 1, Wo = W - w + 1;
-        const int pw_al = (pw + 7) & ~7, s = pw_al - pw;
-        f32x4 acc[NTW];
+        const int na = win_na(h), nb = win_nb(w), s = win_s(w);
+        f32x4 acc[NACC];
 #pragma unroll
-        for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if (row_live) {
-            const int rb = tr * 16 + l16 + hg - ph;  // LDS row of output row (yb0 + 16 tr + l16) at i = 0
+        for (int t = 0; t < NACC; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (yb0 + rq0 < yb1) {
+            // staged row / column of this lane's B chunk at window (0, 0), accumulator 0
+            const int rbase = rq0 + 2 * pr + g + hg - ph;
+            const int cbase = 8 * pc + MPADL - pw - s;
             const char *arow = reinterpret_cast<const char *>(trows) +
-                               ((int64_t)a.C * roff + (int64_t)c * h * tsplit_nk(w)) * 2 * AFRAG + lane * 16;
-            if (16 + s + w - 1 <= 32)
-                mfma_unit<NTW, 1, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
-            else
-                mfma_unit<NTW, 2, WPR, PM>(acc, Fh, Fl, SB, rb, h, arow, tcol0, pw_al, g);
+                               ((int64_t)a.C * roff + (int64_t)c * na * nb) * 2 * AFRAG + lane * 16;
+            mfma_unit<NRQ, NCG, PM>(acc, Fh + rbase * SB, Fl + rbase * SB, 2 * cbase, band_swz<SB>(rbase), na, nb,
+                                    arow);
         }
         // ---- epilogue: exact unscale, correctly rounded /(h*w), scale, pad mask
         const float inv = ldexpf(1.0f, ef + et);  // 1 / (sf * st)
@@ -862,12 +907,15 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                     : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)uo * a.C + c) * plane)
                          : outp + ((size_t)uo * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
-        const int y = yb0 + tr * 16 + l16;
-        if (row_live && y < yb1) {
+#pragma unroll
+        for (int tq = 0; tq < NRQ; ++tq) {
+            const int y = yb0 + rq0 + 4 * tq + 2 * pr + (g >> 1);
+            if (y >= yb1) continue;
             const bool vy = y >= ph && y < ph + Ho;
 #pragma unroll
-            for (int t = 0; t < NTW; ++t) {
-                const int x = (tcol0 + WPR * t) * 16 + 4 * g;
+            for (int tc = 0; tc < NCG; ++tc) {
+                const int t = tq * NCG + tc;
+                const int x = 64 * tc + 8 * pc + 4 * (g & 1);
                 float r4[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -889,13 +937,6 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
         if (umax) unit_max_wave(vmax, u - u_beg, slots, a.out_absmax + uo);
     }
     if (umax) unit_max_flush(slots, units, u_beg, u_end - u_beg, a.out_absmax);
-}
-
-// smallest LDS row stride >= bytes with stride = 32 mod 64 (conflict-free B reads)
-static int mfma_row_stride(int bytes) {
-    int sb = (bytes + 63) / 64 * 64 + 32;
-    if (sb - 64 >= bytes) sb -= 64;
-    return sb;
 }
 
 // squeeze (template_matching.py:34-35): sum over channels, pad, scale
@@ -948,73 +989,69 @@ __global__ void xcorr_squeeze_kernel(const float *__restrict__ work, const tmr_u
 static constexpr int kMfmaMinK = 1;
 
 static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
-    if (W % 32 != 0 || W > 256 || max_ht > 31 || max_wt > 31 || H < 1) return false;
-    const int LR = 32 + 2 * (max_ht / 2);
+    if (W % 64 != 0 || W > 256 || max_ht > 31 || max_wt > 31 || H < 1) return false;
+    const int LR = 32 + 2 * (max_ht / 2) + WIN_OVER;
     return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
 }
 
-template <int NTW, int NV4, int TRB, int PM, bool OB>
+template <int NRQ, int NCG, int PM, bool OB>
 static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp) {
-    const void *kfn = (const void *)xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>;
+    const void *kfn = (const void *)xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB>;
     if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
-    hipLaunchKernelGGL((xcorr_mfma_kernel<NTW, NV4, TRB, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows, texp,
-                       a.out, a.units);
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
+                       texp, a.out, a.units);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
 }
 
-template <int TRB, int PM, bool OB = false>
+template <int NRQ, int PM, bool OB = false>
 static int launch_mfma_w(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
-                         const _Float16 *trows, const int32_t *texp, int nv4) {
-    const int ntw = a.W / 16 / (4 / TRB);
-    switch (ntw) {
-#define TMR_NTW(K)                                                                             \
-    case K:                                                                                    \
-        return nv4 == 8 ? launch_mfma_t<K, 8, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp)    \
-                        : launch_mfma_t<K, 16, TRB, PM, OB>(a, m, lds, nblk, s, trows, texp);
-        TMR_NTW(1) TMR_NTW(2) TMR_NTW(3) TMR_NTW(4) TMR_NTW(6) TMR_NTW(8) TMR_NTW(12)
-#undef TMR_NTW
+                         const _Float16 *trows, const int32_t *texp) {
+    switch (a.W / 64) {  // 64-column accumulator groups per row quad
+        case 1: return launch_mfma_t<NRQ, 1, PM, OB>(a, m, lds, nblk, s, trows, texp);
+        case 2: return launch_mfma_t<NRQ, 2, PM, OB>(a, m, lds, nblk, s, trows, texp);
+        case 3: return launch_mfma_t<NRQ, 3, PM, OB>(a, m, lds, nblk, s, trows, texp);
+        case 4: return launch_mfma_t<NRQ, 4, PM, OB>(a, m, lds, nblk, s, trows, texp);
         default: return TMR_E_UNSUPPORTED;
     }
 }
 
-template <int TRB>
+template <int NRQ>
 static int launch_mfma_p(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
-                         const _Float16 *trows, const int32_t *texp, int nv4, int prec, bool out16) {
+                         const _Float16 *trows, const int32_t *texp, int prec, bool out16) {
     if (out16)
-        return prec == TMR_PREC_BF16 ? launch_mfma_w<TRB, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp, nv4)
+        return prec == TMR_PREC_BF16 ? launch_mfma_w<NRQ, TMR_PREC_BF16, true>(a, m, lds, nblk, s, trows, texp)
                                      : TMR_E_UNSUPPORTED;
     switch (prec) {
-        case TMR_PREC_F16X3: return launch_mfma_w<TRB, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp, nv4);
-        case TMR_PREC_BF16: return launch_mfma_w<TRB, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp, nv4);
-        case TMR_PREC_F16: return launch_mfma_w<TRB, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp, nv4);
+        case TMR_PREC_F16X3: return launch_mfma_w<NRQ, TMR_PREC_F16X3>(a, m, lds, nblk, s, trows, texp);
+        case TMR_PREC_BF16: return launch_mfma_w<NRQ, TMR_PREC_BF16>(a, m, lds, nblk, s, trows, texp);
+        case TMR_PREC_F16: return launch_mfma_w<NRQ, TMR_PREC_F16>(a, m, lds, nblk, s, trows, texp);
         default: return TMR_E_INVALID;
     }
 }
 
-// Band height: 64 output rows (4 tile rows, one per wave, every tile column
-// of the row per wave) when the band and its halo fit the staging registers
-// and the row is 8 or 12 tiles wide; else 32 rows (2 tile rows, 2 waves per
-// row).  Measured (round 6, kbench_xcorr, one box, two reps): config-B mix
-// 4.77 / 4.75 -> 4.42 / 4.45 ms (fp32, 3 terms), config-C mix 3.22 / 3.20 ->
-// 2.80 / 2.77 ms (one bf16 term): half the bands, so half the A-fragment
-// fetches and halo re-stages per output, 8-12 independent accumulators per
-// wave and three template rows of A prefetch.
-static int band_tiles(int W, int max_ht) {
-    const int64_t lr4 = 64 + 2 * (max_ht / 2);
-    return (lr4 * W <= (int64_t)MAXV4 * NT * 4 && (W / 16 == 8 || W / 16 == 12)) ? 4 : 2;
+// Band height: 64 output rows (each wave 4 row quads) when the band and its
+// halo fit the staging registers, else 32 (2 row quads per wave).  Round 6,
+// row-Toeplitz kernel (kbench_xcorr, one box, two reps): 64-row bands took
+// the config-B mix 4.77 / 4.75 -> 4.42 / 4.45 ms and config C 3.22 / 3.20 ->
+// 2.80 / 2.77 ms -- half the bands, so half the A-fragment fetches and halo
+// re-stages per output.
+static int band_rows(int W, int max_ht, int prec) {
+    const int64_t lr64 = 64 + 2 * (max_ht / 2) + WIN_OVER;
+    const int64_t lds64 = (prec == TMR_PREC_F16X3 ? 2 : 1) * lr64 * band_stride(W / 64);
+    // 64 rows where the band fits the staging registers and two blocks still fit a CU's LDS
+    return lr64 * W <= (int64_t)MAXV4 * NT * 4 && lds64 <= 78 * 1024 ? 64 : 32;
 }
 
-static int launch_mfma(const XArgs &a, hipStream_t s, int B, int max_ht, int max_wt, const void *tmpl_split,
+static int launch_mfma(const XArgs &a, hipStream_t s, int B, int max_ht, const void *tmpl_split,
                        int64_t total_rows, int prec, bool out16) {
     MArgs m;
-    const int trb = band_tiles(a.W, max_ht);
+    m.BR = band_rows(a.W, max_ht, prec);
     m.HG = max_ht / 2;
-    m.LR = 16 * trb + 2 * m.HG;
-    const int nk_max = (16 + 7 + max_wt - 1 + 31) / 32;
-    m.SB = mfma_row_stride(2 * (a.W + MPADL + 32 * nk_max));
-    m.nband = (int)tmr_cdiv(a.H, 16 * trb);
+    m.LR = m.BR + 2 * m.HG + WIN_OVER;
+    m.SB = band_stride(a.W / 64);
+    m.nband = (int)tmr_cdiv(a.H, m.BR);
     const int64_t nlog = (int64_t)m.nband * a.C * B;
     TMR_REQUIRE(nlog < (1LL << 31) - 8);
     m.nlog = (int)nlog;
@@ -1023,9 +1060,8 @@ static int launch_mfma(const XArgs &a, hipStream_t s, int B, int max_ht, int max
     const _Float16 *trows = reinterpret_cast<const _Float16 *>(tmpl_split);
     const int32_t *texp = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(tmpl_split) +
                                                             (int64_t)a.C * total_rows * 2 * AFRAG);
-    const int nv4 = (int)tmr_cdiv((int64_t)m.LR * a.W / 4, NT) <= 8 ? 8 : 16;
-    return trb == 4 ? launch_mfma_p<4>(a, m, lds, nblk, s, trows, texp, nv4, prec, out16)
-                    : launch_mfma_p<2>(a, m, lds, nblk, s, trows, texp, nv4, prec, out16);
+    return m.BR == 64 ? launch_mfma_p<4>(a, m, lds, nblk, s, trows, texp, prec, out16)
+                      : launch_mfma_p<2>(a, m, lds, nblk, s, trows, texp, prec, out16);
 }
 
 int64_t tmr_template_split_bytes(int U, int C, int64_t total_rows) {
@@ -1081,7 +1117,7 @@ extern "C" int tmr_xcorr(const tmr_xcorr_args_t *x, void *stream) {
     if (x->algo == TMR_XCORR_MFMA && !fits) return TMR_E_UNSUPPORTED;
     const bool use_mfma = x->algo == TMR_XCORR_MFMA || (x->algo == TMR_XCORR_AUTO && fits && x->min_k >= kMfmaMinK);
     if (use_mfma) {
-        const int rc = launch_mfma(a, s, B, max_ht, max_wt, x->tmpl_split, x->total_rows, x->prec, x->out_bf16 != 0);
+        const int rc = launch_mfma(a, s, B, max_ht, x->tmpl_split, x->total_rows, x->prec, x->out_bf16 != 0);
         if (rc != TMR_OK) return rc;
     } else {
         TMR_REQUIRE(!x->out_bf16);

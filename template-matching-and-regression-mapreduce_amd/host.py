@@ -66,10 +66,11 @@ def template_sizes(boxes: np.ndarray, H: int, W: int):
     return np.stack([x1, y1, x2, y2], 1).astype(np.float32), ht, wt
 
 
-def tsplit_nk_vec(wt: np.ndarray) -> np.ndarray:
-    pw = np.asarray(wt, np.int64) // 2
-    s = ((pw + 7) & ~7) - pw
-    return np.where(16 + s + np.asarray(wt, np.int64) - 1 <= 32, 1, 2)
+def tsplit_windows_vec(ht: np.ndarray, wt: np.ndarray) -> np.ndarray:
+    """tsplit_windows over arrays of template sizes."""
+    h, w = np.asarray(ht, np.int64), np.asarray(wt, np.int64)
+    s = (-(w // 2)) % 8
+    return ((h + 4) // 4) * ((w + s + 14) // 8)
 
 
 def template_size(box, H: int, W: int) -> Tuple[np.ndarray, int, int]:
@@ -108,18 +109,20 @@ def prototype_box(box, H: int, W: int) -> np.ndarray:
     return b
 
 
-def tsplit_nk(wt: int) -> int:
-    """K blocks of 32 per template row in the MFMA correlation's A fragments
-    (include/tmr.h, tmr_template_split): 1 when the 16-column Toeplitz band of
-    a w-wide template row (shifted by s to a 16-B aligned window) fits 32."""
-    pw = int(wt) // 2
-    s = ((pw + 7) & ~7) - pw
-    return 1 if 16 + s + int(wt) - 1 <= 32 else 2
+def tsplit_windows(ht: int, wt: int) -> int:
+    """A-fragment windows per (unit, channel) of the MFMA correlation
+    (include/tmr.h, tmr_template_split; csrc/xcorr.hip win_count): windows of
+    4 input rows x 8 input columns over the 2 x 8 output patch's input region,
+    ceil((h + 1) / 4) * ceil((w + 7 + s) / 8) with s = (-(w // 2)) mod 8
+    aligning each window's first column to 8 elements (16 B)."""
+    h, w = int(ht), int(wt)
+    s = (-(w // 2)) % 8
+    return ((h + 4) // 4) * ((w + s + 14) // 8)
 
 
 def tsplit_rows(units: np.ndarray) -> int:
-    """total_rows of tmr_template_split: sum of ht * tsplit_nk(wt)."""
-    return int(sum(int(h) * tsplit_nk(int(w)) for h, w in zip(units["ht"], units["wt"])))
+    """total_rows of tmr_template_split: the sum of tsplit_windows over the units."""
+    return int(sum(tsplit_windows(h, w) for h, w in zip(units["ht"], units["wt"])))
 
 
 SMALL_UNITS = 8  # up to this many units build_units runs per unit
@@ -141,7 +144,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
         units["ht"], units["wt"] = ht, wt
         sizes = C * ht * wt
         units["tmpl_offset"] = np.concatenate([[0], np.cumsum(sizes)[:-1]])
-        rows = ht * tsplit_nk_vec(wt)
+        rows = tsplit_windows_vec(ht, wt)
         units["row_offset"] = np.concatenate([[0], np.cumsum(rows)[:-1]])
         return units, int(sizes.sum()), max(1, int(ht.max())), max(1, int(wt.max()))
     # per unit (prototype templates, and few units: the module API's one
@@ -158,7 +161,7 @@ def build_units(boxes: np.ndarray, images: Sequence[int], H: int, W: int, C: int
             roi, ht, wt = (0.0, 0.0, 0.0, 0.0), 1, 1
         units[u] = (int(images[u]), ttype, ht, wt, roi, pbox, off, rows, 0)
         off += C * ht * wt
-        rows += ht * tsplit_nk(wt)
+        rows += tsplit_windows(ht, wt)
         max_ht, max_wt = max(max_ht, ht), max(max_wt, wt)
     return units, off, max_ht, max_wt
 

@@ -170,7 +170,7 @@ def _xcorr(feature: torch.Tensor, template: torch.Tensor, scale: torch.Tensor,
     units["image"] = np.arange(bs)
     units["ht"], units["wt"] = h, w
     units["tmpl_offset"] = np.arange(bs) * (C * h * w)
-    units["row_offset"] = np.arange(bs) * h * host.tsplit_nk(w)
+    units["row_offset"] = np.arange(bs) * host.tsplit_windows(h, w)
     dev = feature.device
     ud = _units_to_device(units, dev)
     iu = _h2d(np.arange(bs + 1, dtype=np.int32), dev)

@@ -341,7 +341,7 @@ def test_build_units_vectorised_matches_scalar():
         assert units["tmpl_offset"][u] == off and units["row_offset"][u] == rows
         assert units["pad_"][u] == 0
         off += C * ht * wt
-        rows += ht * host.tsplit_nk(wt)
+        rows += host.tsplit_windows(ht, wt)
     assert tfl == off and mh == units["ht"].max() and mw == units["wt"].max()
     with pytest.raises(ValueError):
         host.build_units(np.array([[0.5, 0.5, 0.5, 0.5]], np.float32), [0], H, W, C)

@@ -1074,17 +1074,18 @@ def test_reduced_precision_forward_vs_oracle(prec):
 
 
 # ----------------------------------------------------------------- xcorr (MFMA)
-@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15), (70, 128, 8, 31),
-                                        (192, 192, 8, 31), (33, 32, 8, 15), (128, 128, 8, 15),
-                                        (100, 192, 8, 21), (77, 128, 8, 9)])
+@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 64, 24, 15), (70, 128, 8, 31),
+                                        (192, 192, 8, 31), (33, 64, 8, 15), (128, 128, 8, 15),
+                                        (100, 192, 8, 21), (77, 256, 8, 9), (40, 256, 8, 29)])
 def test_xcorr_mfma_vs_oracle(H, W, C, kmax):
     """The row-Toeplitz MFMA correlation kernel (TMR_XCORR_MFMA, 3-term fp16
     split) against the C oracle at every odd template side 1..31, rectangular
     templates, several units per image, band edges (H % 32 / % 64 != 0), a
     learned scale, relu output, the fused max |f_TM| and the zero pad border.
     Both band heights run: 64-row bands where the band and halo fit the
-    staging registers and a row is 8 or 12 tiles (W 128 / 192, kmax <= 21 at
-    192), 32-row bands otherwise (W 96 / 32, kmax 31 at 192)."""
+    staging registers (W 64 / 128, W 192 with kmax <= 21, W 256 with kmax <=
+    1), 32-row bands otherwise; every accumulator width (1-4 64-column
+    groups)."""
     _xcorr_mfma_case(H, W, C, kmax, "fp32")
 
 
@@ -1096,7 +1097,7 @@ XCORR_ONE_TERM_TOL = {"bf16": 1e-2, "f16": 2e-3}
 
 
 @pytest.mark.parametrize("prec", ["bf16", "f16"])
-@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 96, 24, 15), (128, 128, 8, 15),
+@pytest.mark.parametrize("H,W,C,kmax", [(128, 128, 16, 31), (70, 64, 24, 15), (128, 128, 8, 15),
                                         (100, 192, 8, 21)])
 def test_xcorr_mfma_one_term_vs_oracle(H, W, C, kmax, prec):
     """tmr_xcorr with one bf16 / fp16 MFMA term: the same shapes, border,
@@ -1212,6 +1213,27 @@ def test_engine_bf16_ftm_plane_bitexact():
         # the module form (relu(f_TM) returned) keeps the fp32 plane
         eng.forward_units(cuda(feats), ui, ex.reshape(-1, 4), want_aux=True)
         assert not eng.last_xcorr_out16
+
+
+def test_xcorr_mfma_refuses_other_widths():
+    """The MFMA correlation runs W % 64 == 0 (64-column accumulator groups):
+    another width is TMR_E_UNSUPPORTED under TMR_XCORR_MFMA, and the engine's
+    cost model ('auto') runs the VALU kernel there."""
+    C, H, W = 8, 40, 96
+    f = synth.normal(6, (1, C, H, W))
+    boxes = np.stack([synth.exemplar_box(k, H, W, 5, 7) for k in (5, 13)])
+    P = {"matcher.scale": torch.tensor([1.0], device=DEV)}
+    eng = tmr_amd.TMREngine(P, tmr_amd.PathConfig(emb_dim=C))
+    eng.xcorr_algo = "mfma"
+    with pytest.raises(tmr_amd.TMRError):
+        eng.match(cuda(f), [0, 0], boxes)
+    eng.xcorr_algo = "auto"
+    out, _ = eng.match(cuda(f), [0, 0], boxes)
+    assert eng.last_xcorr_algo == "valu"
+    for u in range(2):
+        roi, ht, wt = oracle.template_size(boxes[u], H, W)
+        ref = oracle.xcorr(f[0], oracle.roi_align(f[0], roi, ht, wt), 1.0)
+        assert normwise(out[u].cpu().numpy(), ref) <= TOL
 
 
 def test_xcorr_mfma_squeeze_and_engine():
