@@ -541,9 +541,6 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
 // rows meet in that XCD's L2.
 constexpr int MPADL = 16;   // zero fp16 columns left of the image (>= pw + s = 16 at most)
 constexpr int MPADR = 24;   // zero fp16 columns right of the image (>= pw + 7)
-// A-fragment prefetch distance in windows: the 3-term kernel's windows are
-// 3 MFMAs per accumulator, the one-term kernel's 1
-constexpr int XCORR_PF3 = 2, XCORR_PF1 = 4;
 constexpr int MAXV4 = 16;   // staged float4 per thread (LR * W <= 16384)
 // The last window row block of a template reaches up to 3 rows past the
 // h + 1 input rows of a 2-row patch (4 ceil((h + 1) / 4) >= h + 1); its A
@@ -671,7 +668,7 @@ __global__ __launch_bounds__(256) void template_split_kernel(const float *__rest
                 const int j = 8 * b + q - cc - s;
                 x[q] = (i >= 0 && i < h && j >= 0 && j < w) ? t[i * w + j] * st : 0.0f;
             }
-            char *f = dst + (size_t)((a * nb + b) * 2) * AFRAG;
+            char *f = dst + (size_t)((b * na + a) * 2) * AFRAG;  // column-major: mfma_unit's order
             if (bf) {  // wave-uniform: bf16 hi (the one-term bf16 MFMA reads hi only)
                 b8 hi;
 #pragma unroll
@@ -732,56 +729,70 @@ __device__ __forceinline__ int lds_off(int lr, int col) {  // col % 4 == 0 (elem
 template <int NRQ, int NCG, int PM>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NRQ * NCG], const char *rh, const char *rl, int cb, int swz,
                                           int na, int nb, const char *arow) {
+    // Windows are walked column by column (b outer, a inner).  Accumulator
+    // row-quad tq at window row a reads band row-quad a + tq, so within a
+    // column each staged chunk serves NRQ accumulators at NRQ consecutive
+    // windows: the chunks live in a rolling set of NRQ row slots and a window
+    // step reads ONE new row-quad per column group from LDS (NCG chunks per
+    // plane instead of NRQ * NCG).  The a loop is unrolled by UA (a multiple
+    // of NRQ) so every slot index is static; the A fragment of slot j is
+    // prefetched UA windows ahead along the column, wrapping to row j of the
+    // next column.
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int PF = SPLIT ? XCORR_PF3 : XCORR_PF1;  // (windows)
+    constexpr int UA = 4;
     constexpr int SB = band_stride(NCG);
-    constexpr int NACC = NRQ * NCG;
-    const int nw = na * nb;
-    V ah[PF], al[PF];
     auto afrag = [&](int wi, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)(wi * 2 + term) * AFRAG);
     };
+    V ah[UA], al[UA];
+    // (every prefetch loads SOME fragment of the unit -- a clamped index, not a
+    // branch -- so the loads stay in flight across the window steps instead of
+    // being waited for at a branch join)
+    const int wlast = na * nb - 1;
 #pragma unroll
-    for (int p = 0; p < PF; ++p)
-        if (p < nw) {
-            ah[p] = afrag(p, 0);
-            if (SPLIT) al[p] = afrag(p, 1);
+    for (int j = 0; j < UA; ++j) {
+        ah[j] = afrag(min(j, wlast), 0);
+        if (SPLIT) al[j] = afrag(min(j, wlast), 1);
+    }
+    V xb[NRQ][NCG], xl[NRQ][NCG];
+    auto load_row = [&](V (&hb)[NCG], V (&lb)[NCG], int row, int cw) {
+#pragma unroll
+        for (int tc = 0; tc < NCG; ++tc) {
+            const int o = row * 4 * SB + ((cw + 128 * tc) ^ swz);
+            hb[tc] = *reinterpret_cast<const V *>(rh + o);
+            if (SPLIT) lb[tc] = *reinterpret_cast<const V *>(rl + o);
         }
-    int a = 0, b = 0;
-    for (int w0 = 0; w0 < nw; w0 += PF) {
+    };
+    for (int b = 0; b < nb; ++b) {
+        const int cw = cb + 16 * b;
 #pragma unroll
-        for (int p = 0; p < PF; ++p) {
-            const int wi = w0 + p;
-            if (wi >= nw) break;
-            const int ro = a * 4 * SB, cw = cb + 16 * b;
-            V xb[NACC], xl[NACC];
+        for (int j = 0; j < NRQ - 1; ++j) load_row(xb[j], xl[j], j, cw);
+        for (int a0 = 0; a0 < na; a0 += UA) {
 #pragma unroll
-            for (int tc = 0; tc < NCG; ++tc) {
-                const int c0 = ro + ((cw + 128 * tc) ^ swz);
+            for (int j = 0; j < UA; ++j) {
+                const int a = a0 + j;
+                if (a >= na) break;
+                load_row(xb[(j + NRQ - 1) % NRQ], xl[(j + NRQ - 1) % NRQ], a + NRQ - 1, cw);
 #pragma unroll
-                for (int tq = 0; tq < NRQ; ++tq) {
-                    const int o = c0 + tq * 4 * SB;
-                    xb[tq * NCG + tc] = *reinterpret_cast<const V *>(rh + o);
-                    if (SPLIT) xl[tq * NCG + tc] = *reinterpret_cast<const V *>(rl + o);
-                }
+                for (int tq = 0; tq < NRQ; ++tq)
+#pragma unroll
+                    for (int tc = 0; tc < NCG; ++tc) {
+                        const int t = tq * NCG + tc;
+                        const V &bh = xb[(j + tq) % NRQ][tc];
+                        acc[t] = xmma(ah[j], bh, acc[t]);
+                        if (SPLIT) {
+                            acc[t] = xmma(ah[j], xl[(j + tq) % NRQ][tc], acc[t]);
+                            acc[t] = xmma(al[j], bh, acc[t]);
+                        }
+                    }
+                // the slot's next fragment (UA rows down, else row j of the next
+                // column) lands in the registers just consumed: no copy at the
+                // loop back edge, so nothing waits for it before its use
+                const int wn = min(a + UA < na ? b * na + a + UA : (b + 1) * na + j, wlast);
+                ah[j] = afrag(wn, 0);
+                if (SPLIT) al[j] = afrag(wn, 1);
             }
-            const V ch = ah[p];
-            V cl;
-            if (SPLIT) cl = al[p];
-            if (wi + PF < nw) {
-                ah[p] = afrag(wi + PF, 0);
-                if (SPLIT) al[p] = afrag(wi + PF, 1);
-            }
-#pragma unroll
-            for (int t = 0; t < NACC; ++t) {
-                acc[t] = xmma(ch, xb[t], acc[t]);
-                if (SPLIT) {
-                    acc[t] = xmma(ch, xl[t], acc[t]);
-                    acc[t] = xmma(cl, xb[t], acc[t]);
-                }
-            }
-            if (++b == nb) { b = 0; ++a; }
         }
     }
 }
