@@ -67,6 +67,15 @@ def groups(d, lines, reps):
     return res
 
 
+def _buildinfo():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "tmr_buildinfo", os.path.join(REPO, "template-matching-and-regression-mapreduce_amd", "buildinfo.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def mean(xs):
     return sum(xs) / len(xs) if xs else None
 
@@ -110,11 +119,15 @@ def main(sweep, label, reps=3):
     for d in sorted(glob.glob(os.path.join(sweep, "*"))):
         if os.path.isdir(d) and os.path.exists(os.path.join(d, "kbench.jsonl")):
             out["regimes"][os.path.basename(d)] = regime(d, reps)
+    # the sources the swept kernels were built from: a kernel edit without a
+    # re-sweep turns tests/test_abi_host.py's digest check red
+    digest = _buildinfo().source_digest("xcorr")
+    out["source_digest"] = digest
     with open(os.path.join(HERE, "xcorr_crossover.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     # the engine's table: per regime and algo, ms per launch by k
     cost = {"source": f"profiles/xcorr_crossover.json (rocprofv3 kernel trace, round {label})",
-            "regimes": {}}
+            "source_digest": digest, "regimes": {}}
     for name, per in out["regimes"].items():
         t = {}
         for key, r in per.items():

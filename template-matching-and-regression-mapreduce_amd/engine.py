@@ -73,17 +73,17 @@ class PathConfig:
 # the committed rocprofv3 sweep (xcorr_cost.json, below): kernel-trace
 # durations of both kernels per k in the two regimes, beside each point's
 # counted HBM bytes and MFMA busy (profiles/xcorr_crossover.json; DESIGN.md
-# 4.3).  The constants here are the round-2 HIP-event tables it replaced
-# (kbench_xcorr, profiles/archive/r02w_sweep{128,192}.jsonl), as ms per unit at the
-# 512 x 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
+# 4.3), re-swept whenever xcorr.hip changes (its source digest is recorded and
+# tests/test_abi_host.py fails on a stale one).  The constants here are the
+# round-2 HIP-event tables it replaced (kbench_xcorr,
+# profiles/archive/r02w_sweep{128,192}.jsonl), as ms per unit at the 512 x
+# 128^2 map size, in two exemplar-count regimes: E = 3 (64 images x 3
 # exemplars at 128^2; the image's band staging is shared by 3 units) and
 # E = 16 (8 images x 16 exemplars at 192^2, times / 2.25 for the area).
 # "auto" interpolates the regimes in log E, sums the per-unit costs of a
-# launch (linear in k in between) and runs the cheaper kernel: at E = 3 the
-# VALU kernel wins for k <= 9 and the MFMA kernel for k >= 11 (the
-# crossover); at E = 16 MFMA wins from k = 9 on.  Under the bf16 contract
-# (precision "bf16"/"f16": one 16-bit MFMA term, tmr_xcorr prec) the MFMA
-# kernel wins from k = 5 at E = 3 (profiles/archive/r02af_*).
+# launch (linear in k in between) and runs the cheaper kernel.  Round-6
+# sweep (2-D window MFMA kernel): fp32 MFMA wins from k = 7 in both regimes;
+# one bf16 term from k = 5 at E = 3 and at every k at E = 16.
 XCORR_COST_K = (1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 21, 23, 25, 27, 29, 31)
 _T128 = {  # ms per 192 units (E = 3), r02w sweep (aligned A fragments)
     "valu": (1.720, 1.849, 2.498, 3.174, 4.051, 5.281, 6.538, 8.069, 10.139, 12.159, 14.558, 16.630, 20.469, 23.479, 26.392, 29.846),
@@ -145,14 +145,14 @@ _swept = _load_xcorr_cost()
 if _swept is not None:
     XCORR_COST, XCORR_COST_SOURCE = _swept
 # A mixed-size MFMA launch stages every band with the LARGEST template's halo
-# rows, and its band staging (fp32 -> fp16 hi/lo planes) is shared by fewer
-# units when an image has few of them: measured 1.13x the per-k sum at the
-# config-B 3..15 mix with 3 units per image (5.57 ms vs 4.91,
-# profiles/archive/r02b_kbench_xcorr_mixB*; 1.10x after the aligned-fragment change,
-# 4.75 vs 4.30, profiles/archive/r02w_mixB.jsonl), 1.46x for the k >= 11 units of that
-# batch (~2 per image; profiles/archive/r02c_bench_B* by_class); the VALU kernel's
-# mixes run 1.00-1.04x its per-k sums.  Empirical: 1 + 0.4 / units-per-image.
-XCORR_MFMA_MIX = 0.4
+# rows (and that template's band height), and its band staging is shared by
+# fewer units when an image has few of them.  Rounds 2-5 (row-Toeplitz
+# kernel): 1.10-1.13x the per-k sum at the config-B 3..15 mix (profiles/
+# archive/r02w_mixB.jsonl).  Round 6 (2-D window kernel, rolling band rows):
+# 1.04x (3.764 ms mix vs 3.619 ms per-k mean, one run on one box,
+# profiles/r06_xcorr_rolling).
+# Empirical: 1 + MIX / units-per-image.
+XCORR_MFMA_MIX = 0.12
 
 
 def xcorr_choice(ht: np.ndarray, wt: np.ndarray, units_per_image: float, mfma_ok: bool,

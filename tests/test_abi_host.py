@@ -295,8 +295,8 @@ def test_template_matching_members():
 def test_xcorr_cost_table_committed_crossovers(tmp_path):
     """the live correlation cost model is the committed rocprof
     sweep (xcorr_cost.json), with the crossovers DESIGN.md §4.3 documents
-    (single-size launches: 128^2 E=3 fp32 from k=11, one-term from k=5;
-    192^2 E=16 fp32 from k=7, one-term from k=5); a malformed or incomplete
+    (single-size launches, round-6 sweep: 128^2 E=3 fp32 from k=7, one-term
+    from k=5; 192^2 E=16 fp32 from k=7, one-term at every k); a malformed or incomplete
     table raises instead of silently moving them."""
     import json
     from tmr_amd import engine as e
@@ -305,8 +305,8 @@ def test_xcorr_cost_table_committed_crossovers(tmp_path):
     def first_mfma(upi, one):
         return min(k for k in range(1, 32, 2)
                    if e.xcorr_choice(np.full(8, k), np.full(8, k), upi, True, one) == "mfma")
-    assert first_mfma(3, False) == 11 and first_mfma(3, True) == 5
-    assert first_mfma(16, False) == 7 and first_mfma(16, True) == 5
+    assert first_mfma(3, False) == 7 and first_mfma(3, True) == 5
+    assert first_mfma(16, False) == 7 and first_mfma(16, True) == 1
     bad = tmp_path / "bad.json"
     bad.write_text("{not json")
     with pytest.raises(tmr_amd.TMRError, match="malformed"):
@@ -318,6 +318,23 @@ def test_xcorr_cost_table_committed_crossovers(tmp_path):
     with pytest.raises(tmr_amd.TMRError, match="lacks"):
         e._load_xcorr_cost(str(part))
     assert e._load_xcorr_cost(str(tmp_path / "absent.json")) is None
+
+
+def test_xcorr_cost_table_matches_kernel_sources():
+    """the committed cost table (xcorr_cost.json) and its
+    counter record (profiles/xcorr_crossover.json) were swept on the
+    correlation kernel sources of this tree (buildinfo digest of xcorr.hip,
+    tmr_common.h, Makefile): a kernel edit without re-running
+    profiles/gpu_xcorr_sweep.sh turns this red, so the crossover can never
+    be priced on a kernel that no longer exists."""
+    import json
+    from tmr_amd import buildinfo
+    from tmr_amd import engine as e
+    want = buildinfo.source_digest("xcorr")
+    cost = json.load(open(e._COST_JSON))
+    rec = json.load(open(os.path.join(REPO, "profiles", "xcorr_crossover.json")))
+    assert cost.get("source_digest") == want, "xcorr_cost.json is from other sources: re-run gpu_xcorr_sweep.sh"
+    assert rec.get("source_digest") == want
 
 
 def test_build_units_vectorised_matches_scalar():
