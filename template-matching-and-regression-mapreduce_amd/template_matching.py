@@ -141,9 +141,12 @@ class TemplateMatching(nn.Module):
         if scale is None:
             scale = torch.ones(1, device=sample.device, dtype=torch.float32)
         eng = TMREngine({"matcher.scale": scale}, cfg)
-        # one kernel for the whole launch: the batched matcher equals its own
-        # cross_correlation member bit for bit when the cost model picks the
-        # VALU kernel, as the member runs
+        # the fp32 VALU kernel, as the cross_correlation member runs: the batched
+        # matcher then equals the reference's member loop bit for bit whatever
+        # the template sizes (the cost model's MFMA choice depends on the whole
+        # launch's mix, so a per-image member call could pick the other kernel).
+        # The detection path (MatchingNet -> TMREngine) keeps the cost model.
+        eng.xcorr_algo = "valu"
         out, _ = eng.match(sample.float().contiguous(), list(range(B)), boxes)
         return out
 
