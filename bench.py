@@ -499,7 +499,7 @@ def main():
         xs = float(np.mean(xc_ms)) / 1e3
         xk = eng.last_xcorr_algo
         out["roofline_xcorr"] = {
-            "kernel": ("tmr_xcorr MFMA (xcorr_mfma_kernel: row-Toeplitz implicit GEMM on "
+            "kernel": ("tmr_xcorr MFMA (xcorr_mfma_kernel: 2-D window Toeplitz implicit GEMM on "
                        + ("v_mfma_f32_16x16x32_f16, 3-term fp16 split)" if prec == "fp32" else
                           "v_mfma_f32_16x16x32_%s, one %s term)" % (("bf16", "bf16") if prec == "bf16"
                                                                      else ("f16", "scaled fp16")))

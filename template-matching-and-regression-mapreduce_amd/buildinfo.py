@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import re
 
 _CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
 _COMMON = ("tmr_common.h", "Makefile")
@@ -21,11 +22,23 @@ KERNEL_SOURCES = {
 }
 
 
+def _code(name: str, text: bytes) -> bytes:
+    """The code of a source file: C/C++ comments (and Makefile comment lines)
+    removed and whitespace runs collapsed, so a comment-only edit keeps the
+    digest and any code edit changes it."""
+    if name == "Makefile":
+        text = re.sub(rb"(?m)^\s*#[^\n]*$", b"", text)
+    else:
+        text = re.sub(rb"//[^\n]*|/\*.*?\*/", b" ", text, flags=re.S)
+    return b" ".join(text.split())
+
+
 def source_digest(role: str) -> str:
-    """SHA-256 (hex, first 16 digits) over the role's source files."""
+    """SHA-256 (hex, first 16 digits) over the code of the role's source
+    files (comments and whitespace layout excluded)."""
     h = hashlib.sha256()
     for name in KERNEL_SOURCES[role]:
         h.update(name.encode() + b"\0")
         with open(os.path.join(_CSRC, name), "rb") as fh:
-            h.update(fh.read())
+            h.update(_code(name, fh.read()))
     return h.hexdigest()[:16]

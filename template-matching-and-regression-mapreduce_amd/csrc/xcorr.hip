@@ -531,6 +531,11 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
 // residuals ~2^-22 relative), then exactly unscaled, divided by fl32(h*w)
 // correctly rounded and scaled like the VALU kernels.
 //
+// Measured (kbench_xcorr incl. tmr_template_split, one box): config-B mix
+// 4.42 ms (round-5 row Toeplitz, 64-row bands) -> 4.19 (windows) -> 3.76
+// (rolling band rows, mfma_unit); config E mix 15.0 -> 11.4 -> 9.66 ms; C
+// 2.78 -> 2.72 -> 2.43 ms (profiles/r06_xcorr_window, r06_xcorr_rolling).
+//
 // Block = (band of BR output rows, channel, image), 4 waves; the band's input
 // rows (+- the image's largest template half height, zero rows outside the
 // image, zero columns left/right) are staged ONCE as fp16 hi/lo planes and
@@ -1047,7 +1052,11 @@ static int launch_mfma_p(const XArgs &a, const MArgs &m, size_t lds, unsigned nb
 // row-Toeplitz kernel (kbench_xcorr, one box, two reps): 64-row bands took
 // the config-B mix 4.77 / 4.75 -> 4.42 / 4.45 ms and config C 3.22 / 3.20 ->
 // 2.80 / 2.77 ms -- half the bands, so half the A-fragment fetches and halo
-// re-stages per output.
+// re-stages per output.  The window kernel adds the LDS rule: a 64-row band
+// whose two planes exceed 78 KB leaves one block per CU -- config E at k = 15
+// (192 columns) 6.77 ms at 64 rows vs 5.40 at 32; where two blocks fit, 64
+// rows (E k = 3: 2.83 vs 3.13 ms; config C 2.49 vs 2.86; config B equal,
+// profiles/archive/r06/brexp).
 static int band_rows(int W, int max_ht, int prec) {
     const int64_t lr64 = 64 + 2 * (max_ht / 2) + WIN_OVER;
     const int64_t lds64 = (prec == TMR_PREC_F16X3 ? 2 : 1) * lr64 * band_stride(W / 64);
