@@ -94,6 +94,18 @@ def test_pmc_fields_tied_to_kernel_sources(tmp_path, monkeypatch):
     assert b.load_pmc("C", "heads") == (None, "no PMC record for this config")
 
 
+def test_source_digest_ignores_comments_only():
+    """The digest hashes the code: a comment or layout edit keeps it, any
+    token change moves it."""
+    from tmr_amd import buildinfo
+    a = b"int f(int x) { // twice\n  return 2 * x; /* doubled */ }\n"
+    assert buildinfo._code("k.hip", a) == buildinfo._code("k.hip", b"int f(int x) {\n return 2 * x; }")
+    assert buildinfo._code("k.hip", a) != buildinfo._code("k.hip", a.replace(b"2 * x", b"3 * x"))
+    mk = b"# flags\nHIPFLAGS = -O3\n"
+    assert buildinfo._code("Makefile", mk) == buildinfo._code("Makefile", b"HIPFLAGS = -O3")
+    assert buildinfo._code("Makefile", mk) != buildinfo._code("Makefile", b"HIPFLAGS = -O2")
+
+
 def test_committed_pmc_records_match_this_tree():
     """Every record of the committed profiles/pmc_by_config.json was collected
     on the kernel sources of this tree (so every bench line's traffic /
