@@ -6,8 +6,8 @@
 // 16- / 32-register accumulators; -DCH4=4 for 4), 2 waves per
 // SIMD on every CU.  Per shape: wall (HIP events, best of 5) -> TFLOP/s, and
 // per wave s_memtime ticks -> cycles per MFMA per SIMD.  Prints one JSON line
-// per shape; profiles/mfma_shapes/toeplitz.py turns them into the useful-FLOP
-// table of the Toeplitz formulation.
+// per shape (results/*.jsonl, round 6); profiles/mfma_shapes/toeplitz.py turns
+// them into the useful-FLOP table of the Toeplitz formulations (toeplitz_table.md).
 //
 //   hipcc --offload-arch=gfx950 -O3 mfma_shapes.hip -o mfma_shapes && ./mfma_shapes
 #include <hip/hip_runtime.h>

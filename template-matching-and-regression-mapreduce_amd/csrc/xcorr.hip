@@ -517,8 +517,12 @@ __global__ __launch_bounds__(NT) void xcorr_rows_kernel(XArgs a, const float *__
 // MFMA shape study (profiles/mfma_shapes, round 6: random operands, every
 // 16-bit gfx950 form) found no shape with a better useful rate -- 16x16x16 /
 // 32x32x8 run at 0.65 of 16x16x32's FLOP rate, the 4x4x4 and 16x16x4
-// multi-block forms at 0.31 / 0.36 -- so the geometry, not the instruction,
-// changed.
+// multi-block forms at 0.31 / 0.36; useful rate = useful share x rate per w in
+// profiles/mfma_shapes/toeplitz_table.md) -- so the geometry, not the
+// instruction, changed.  The one exception is the 4x4x4 16-block row form at
+// w <= 5 (192 / 319 useful TFLOP/s vs 154 / 214), where this kernel is bound
+// by its staging, epilogue and stores, not by MFMA issue (k = 3: the MFMA
+// loop is ~1.1 of 2.9 ms, profiles/archive/r06/ablation).
 //
 // The 16 patches of one accumulator tile 4 output rows x 64 columns: patch n
 // at (R + 2 (n >> 3), C0 + 8 (n & 7)).  Lane (n, g) of D holds output row
