@@ -8,6 +8,7 @@ Tolerances (written here):
   (the decode's exp restated through the reference-exp table, exp_table.py)
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -1104,6 +1105,77 @@ def test_xcorr_mfma_one_term_vs_oracle(H, W, C, kmax, prec):
     relu and fused-max contract as the 3-term kernel, at the one-term tolerance;
     the VALU kernel in the same call stays fp32 (1e-5)."""
     _xcorr_mfma_case(H, W, C, kmax, prec)
+
+
+XCORR_SWEEP = int(os.environ.get("TMR_XCORR_SWEEP", "24"))
+
+
+@pytest.mark.parametrize("seed", range(XCORR_SWEEP))
+def test_xcorr_mfma_random_sweep_vs_oracle(seed):
+    """Seeded random sweep of the 2-D window MFMA correlation (round 6) against
+    the C oracle, away from the fixed shapes above: 1-3 images, 1-6 units with
+    random image assignment (images without units included), every
+    accumulator width (W 64 / 128 / 192 / 256), heights 5-160 (band edges at
+    every residue), random odd rectangular templates up to the kernel's
+    staging limit at random positions, feature scales 1e-6 ... 1e6, sparse and
+    constant maps, a random learned scale; fp32 (3-term split, 1e-5 normwise)
+    or one bf16 term (1e-2).  The fused per-unit max and relu output are
+    checked bit for bit against the plane.  TMR_XCORR_SWEEP=N for more."""
+    from tmr_amd._lib import PREC_CODES, XCORR_ALGOS, call, ptr, size, stream, xcorr
+    from tmr_amd.engine import _h2d, _units_to_device
+    r = np.random.default_rng(9000 + seed)
+    B = int(r.integers(1, 4))
+    W = int(r.choice([64, 128, 192, 256]))
+    H = int(r.integers(5, 161))
+    C = int(r.integers(1, 7))
+    prec = "bf16" if r.random() < 0.2 else "fp32"
+    kcap = 29 if W == 256 else 31  # (35 + 2 * (kmax // 2)) * W staged floats <= 16384
+    f = synth.normal(7000 + seed, (B, C, H, W)) * np.float32(10.0 ** r.uniform(-6, 6))
+    kind = r.integers(0, 4)
+    if kind == 1:  # sparse
+        f = f * (synth.uniform(7100 + seed, B * C * H * W).reshape(f.shape) < 0.05)
+    elif kind == 2:  # constant planes
+        f = np.broadcast_to(f[:, :, :1, :1], f.shape).copy()
+    f = np.ascontiguousarray(f, np.float32)
+    U = int(r.integers(1, 7))
+    ui = sorted(int(x) for x in r.integers(0, B, U))
+    boxes = []
+    for u in range(U):
+        kh = int(min(kcap, H // 2 * 2 - 1 if H % 2 == 0 else H, 2 * r.integers(0, 16) + 1))
+        kw = int(min(kcap, 2 * r.integers(0, 16) + 1))
+        boxes.append(synth.exemplar_box(kh, H, W, int(r.integers(0, H - kh + 1)), int(r.integers(0, W - kw + 1)), kw))
+    boxes = np.stack(boxes)
+    units, tfl, mh, mw = host.build_units(boxes, ui, H, W, C)
+    fd = cuda(f)
+    tm = tmr_amd.TemplateMatching("roi_align").to(DEV)
+    tmpl = torch.cat([tm.extract_template(fd[ui[u]:ui[u] + 1], torch.from_numpy(boxes[u])).reshape(-1)
+                      for u in range(U)])
+    ud = _units_to_device(units, DEV)
+    iu = _h2d(host.image_ranges(ui, B), DEV)
+    sc = float(np.float32(r.uniform(0.2, 3.0)))
+    scale = torch.tensor([sc], device=DEV)
+    rows = host.tsplit_rows(units)
+    tsplit = torch.empty(size("template_split", U, C, rows), device=DEV, dtype=torch.uint8)
+    pc = PREC_CODES[prec]
+    call("tmr_template_split", ptr(tmpl), ptr(ud), U, C, rows, pc, ptr(tsplit), stream())
+    out = torch.empty((U, C, H, W), device=DEV)
+    relu = torch.empty_like(out)
+    amax = torch.zeros(U, device=DEV)
+    xcorr(f=ptr(fd), templates=ptr(tmpl), units=ptr(ud), img_units=ptr(iu), scale=ptr(scale), out=ptr(out),
+          relu_out=ptr(relu), out_absmax=ptr(amax), tmpl_split=ptr(tsplit), total_rows=rows, B=B, C=C, H=H, W=W,
+          U=U, max_ht=mh, max_wt=mw, min_k=1, algo=XCORR_ALGOS["mfma"], prec=pc, stream=stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(amax.cpu().numpy(), np.abs(got).reshape(U, -1).max(1))
+    assert np.array_equal(relu.cpu().numpy(), np.maximum(got, 0))
+    tol = TOL if prec == "fp32" else XCORR_ONE_TERM_TOL[prec]
+    tmpl_h = tmpl.cpu().numpy()
+    for u in range(U):
+        ht, wt, off = int(units["ht"][u]), int(units["wt"][u]), int(units["tmpl_offset"][u])
+        t = tmpl_h[off:off + C * ht * wt].reshape(C, ht, wt)
+        ref = oracle.xcorr(f[ui[u]], t, sc)
+        e = normwise(got[u], ref)
+        assert e <= tol, (seed, u, ht, wt, H, W, C, prec, int(kind), e)
 
 
 def _xcorr_mfma_case(H, W, C, kmax, prec):
