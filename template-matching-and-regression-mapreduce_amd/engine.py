@@ -579,6 +579,7 @@ class TMREngine:
         # on the launch stream around the fused decoder kernel (bench.py)
         self.decoder_events = None
         self.xcorr_events = None
+        self.xcorr_split_events = []  # (start, end) of each timed launch's tmr_template_split
         self.last_xcorr_flops = 0.0
         self.last_xcorr_bytes = 0.0
         self.last_xcorr_dram_bytes = 0.0
@@ -832,10 +833,11 @@ class TMREngine:
         # max |f_TM| per unit fused in the kernel (the decoder's per-unit
         # activation scale source)
         slots = torch.zeros(U, device=dev, dtype=torch.float32)
-        ev = None
-        if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream
+        ev = evs = None
+        if self.xcorr_events is not None:  # bench.py: HIP events on the launch stream, around
+            # the correlation kernel alone and, separately, its template split
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
+            evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         min_k = int(min(units["ht"].min(), units["wt"].min()))
         # MFMA operand precision: the fp32 path's 3-term split, or one bf16 /
         # fp16 term under the bf16 contract (config C); the VALU kernels are fp32
@@ -857,7 +859,14 @@ class TMREngine:
             # the MFMA correlation's template operands (per (unit, channel) scale)
             rows = host.tsplit_rows(units)
             tsplit = torch.empty(size("template_split", U, C, rows), device=dev, dtype=torch.uint8)
+            if evs is not None:
+                evs[0].record()
             call("tmr_template_split", ptr(tmpl), ptr(units_d), U, C, rows, pc, ptr(tsplit), stream())
+            if evs is not None:
+                evs[1].record()
+                self.xcorr_split_events.append(evs)
+        if ev is not None:
+            ev[0].record()
         xcorr(f=ptr(fp), templates=ptr(tmpl), units=ptr(units_d), img_units=ptr(img_units_d), scale=ptr(scale),
               out=ptr(out), relu_out=ptr(relu), work=ptr(work), out_absmax=ptr(slots), tmpl_split=ptr(tsplit),
               total_rows=rows, B=B, C=C, H=H, W=W, U=U, max_ht=mh, max_wt=mw, squeeze=int(cfg.squeeze),
