@@ -1173,9 +1173,26 @@ def test_xcorr_mfma_random_sweep_vs_oracle(seed):
     for u in range(U):
         ht, wt, off = int(units["ht"][u]), int(units["wt"][u]), int(units["tmpl_offset"][u])
         t = tmpl_h[off:off + C * ht * wt].reshape(C, ht, wt)
-        ref = oracle.xcorr(f[ui[u]], t, sc)
-        e = normwise(got[u], ref)
-        assert e <= tol, (seed, u, ht, wt, H, W, C, prec, int(kind), e)
+        # the contract is stated against the exact correlation (float64, FFT):
+        # the fp32 oracle's own sequential accumulation over h*w taps drifts by
+        # up to ~1.2e-5 on constant planes (every rounding of equal products
+        # biased one way), past the tolerance it is meant to check
+        exact = _xcorr_exact(f[ui[u]], t, sc)
+        e = normwise(got[u], exact)
+        assert e <= tol, (seed, u, ht, wt, H, W, C, prec, int(kind), e, normwise(oracle.xcorr(f[ui[u]], t, sc), exact))
+
+
+def _xcorr_exact(f, t, scale):
+    """The correlation in float64 (scipy FFT, relative error ~1e-15 of the
+    largest output): zero pad border, / (h*w), * scale; rounded to fp32."""
+    from scipy.signal import fftconvolve
+    C, H, W = f.shape
+    h, w = t.shape[-2:]
+    out = np.zeros((C, H, W), np.float64)
+    for c in range(C):
+        v = fftconvolve(f[c].astype(np.float64), t[c, ::-1, ::-1].astype(np.float64), mode="valid")
+        out[c, h // 2:h // 2 + H - h + 1, w // 2:w // 2 + W - w + 1] = v / (h * w) * float(scale)
+    return out
 
 
 def _xcorr_mfma_case(H, W, C, kmax, prec):
