@@ -981,7 +981,7 @@ __global__ void xpack_kernel(const float *__restrict__ x, int S, int Cin, int Hi
 constexpr int XSEG = 128;
 constexpr int XPACK16_RPB = 4;  // rows per block of the bf16-input record pack (1/4/8: r03s)
 // IN: the activation's element type, float or __bf16 (a bf16 f_TM plane from
-// tmr_xcorr_out: bf16 records of it are its own elements, tmr_split_xpack16);
+// tmr_xcorr with out_bf16: bf16 records of it are its own elements, tmr_split_xpack16);
 // RPB rows of the segment per block (the bf16 form moves half the bytes per
 // row: 4 rows keep as many loads in flight per block).
 template <int PREC, typename IN = float, int RPB = 1>
