@@ -735,7 +735,7 @@ __device__ __forceinline__ int lds_off(int lr, int col) {  // col % 4 == 0 (elem
 // cb + 16 b + 128 tc), then its MFMAs; the A fragments (hi and lo) are
 // aligned 16-B lane loads of the pre-expanded fragments, issued PF windows
 // ahead.
-template <int NRQ, int NCG, int PM>
+template <int NRQ, int NCG, int PM, int UA>
 __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NRQ * NCG], const char *rh, const char *rl, int cb, int swz,
                                           int na, int nb, const char *arow) {
     // Windows are walked column by column (b outer, a inner).  Accumulator
@@ -744,12 +744,11 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NRQ * NCG], const char *r
     // windows: the chunks live in a rolling set of NRQ row slots and a window
     // step reads ONE new row-quad per column group from LDS (NCG chunks per
     // plane instead of NRQ * NCG).  The a loop is unrolled by UA (a multiple
-    // of NRQ) so every slot index is static; the A fragment of slot j is
-    // prefetched UA windows ahead along the column, wrapping to row j of the
-    // next column.
+    // of NRQ, prefetch_windows) so every slot index is static; the A fragment
+    // of slot j is prefetched UA windows ahead along the column, wrapping to
+    // row j of the next column.
     typedef typename XOp<PM>::V8 V;
     constexpr bool SPLIT = XOp<PM>::SPLIT;
-    constexpr int UA = 4;
     constexpr int SB = band_stride(NCG);
     auto afrag = [&](int wi, int term) -> V {
         return *reinterpret_cast<const V *>(arow + (size_t)(wi * 2 + term) * AFRAG);
@@ -809,7 +808,7 @@ __device__ __forceinline__ void mfma_unit(f32x4 (&acc)[NRQ * NCG], const char *r
 // OB: f_TM leaves as bf16 (the bf16 contract's detect path: the decoder's
 // bf16 records are bf16(f_TM) either way, so the fp32 plane is never needed;
 // half the bytes written here and read by the record pack)
-template <int NRQ, int NCG, int NV4, int PM, bool OB = false>
+template <int NRQ, int NCG, int NV4, int PM, bool OB = false, int UA = 4>
 __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const _Float16 *__restrict__ trows,
                                                        const int32_t *__restrict__ texp,
                                                        float *__restrict__ outp,
@@ -916,7 +915,7 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
             const int cbase = 8 * pc + MPADL - pw - s;
             const char *arow = reinterpret_cast<const char *>(trows) +
                                ((int64_t)a.C * roff + (int64_t)c * na * nb) * 2 * AFRAG + lane * 16;
-            mfma_unit<NRQ, NCG, PM>(acc, Fh + rbase * SB, Fl + rbase * SB, 2 * cbase, band_swz<SB>(rbase), na, nb,
+            mfma_unit<NRQ, NCG, PM, UA>(acc, Fh + rbase * SB, Fl + rbase * SB, 2 * cbase, band_swz<SB>(rbase), na, nb,
                                     arow);
         }
         // ---- epilogue: exact unscale, correctly rounded /(h*w), scale, pad mask
@@ -927,6 +926,17 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                     : OB ? reinterpret_cast<float *>(reinterpret_cast<__bf16 *>(outp) + ((size_t)uo * a.C + c) * plane)
                          : outp + ((size_t)uo * a.C + c) * plane;
         float *rp = (a.relu_out && !a.squeeze) ? a.relu_out + ((size_t)uo * a.C + c) * plane : nullptr;
+        // the pad mask without exec-mask blocks: a lane's column validity per
+        // (column group, element) once per unit, its row validity once per row
+        // quad; every element is computed and a pad element selected to 0
+        bool cv[NCG][4];
+#pragma unroll
+        for (int tc = 0; tc < NCG; ++tc)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int xx = 64 * tc + 8 * pc + 4 * (g & 1) + j;
+                cv[tc][j] = xx >= pw && xx < pw + Wo;
+            }
 #pragma unroll
         for (int tq = 0; tq < NRQ; ++tq) {
             const int y = yb0 + rq0 + 4 * tq + 2 * pr + (g >> 1);
@@ -939,8 +949,8 @@ __global__ __launch_bounds__(NT) void xcorr_mfma_kernel(XArgs a, MArgs m, const 
                 float r4[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int xx = x + j;
-                    r4[j] = (vy && xx >= pw && xx < pw + Wo) ? div_cr(acc[t][j] * inv, denom, rden) * sc : 0.0f;
+                    const float v = div_cr(acc[t][j] * inv, denom, rden) * sc;
+                    r4[j] = (vy && cv[tc][j]) ? v : 0.0f;
                     vmax = fmaxf(vmax, fabsf(r4[j]));
                 }
                 if (OB) {
@@ -1014,12 +1024,34 @@ static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
     return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
 }
 
+template <int NRQ, int NCG, int PM, bool OB, int UA>
+static int launch_mfma_u(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
+                         const _Float16 *trows, const int32_t *texp) {
+    const void *kfn = (const void *)xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>;
+    if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
+                       texp, a.out, a.units);
+    TMR_CHECK_LAUNCH();
+    return TMR_OK;
+}
+
+// A-fragment prefetch distance (windows): 8 where the extra 16 (3-term) VGPRs
+// keep the occupancy -- the 2-row-quad, 3-group 3-term kernel (config E's
+// 32-row bands at 192 columns: 168 + 24 registers, 2 waves per SIMD either way
+// once the LDS is counted): E mix 9.12 -> 8.73 ms, k = 31 13.72 -> 13.33
+// (kbench_xcorr, one box, profiles/archive/r06/ua); elsewhere 4 (8 measured
+// equal at B and C and 1.4x slower at E k = 7, whose kernel drops to one wave
+// per SIMD).
+template <int NRQ, int NCG, int PM>
+constexpr int prefetch_windows() { return NRQ == 2 && NCG == 3 && PM == TMR_PREC_F16X3 ? 8 : 4; }
+
 template <int NRQ, int NCG, int PM, bool OB>
 static int launch_mfma_t(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
                          const _Float16 *trows, const int32_t *texp) {
-    const void *kfn = (const void *)xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB>;
+    constexpr int UA = prefetch_windows<NRQ, NCG, PM>();
+    const void *kfn = (const void *)xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>;
     if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
-    hipLaunchKernelGGL((xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
+    hipLaunchKernelGGL((xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
                        texp, a.out, a.units);
     TMR_CHECK_LAUNCH();
     return TMR_OK;
