@@ -1024,17 +1024,6 @@ static bool mfma_fits(int H, int W, int max_ht, int max_wt) {
     return (int64_t)LR * W <= (int64_t)MAXV4 * NT * 4;
 }
 
-template <int NRQ, int NCG, int PM, bool OB, int UA>
-static int launch_mfma_u(const XArgs &a, const MArgs &m, size_t lds, unsigned nblk, hipStream_t s,
-                         const _Float16 *trows, const int32_t *texp) {
-    const void *kfn = (const void *)xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>;
-    if (lds > 64 * 1024 && tmr_set_max_lds(kfn, lds) != hipSuccess) return TMR_E_HIP;
-    hipLaunchKernelGGL((xcorr_mfma_kernel<NRQ, NCG, MAXV4, PM, OB, UA>), dim3(nblk), dim3(NT), lds, s, a, m, trows,
-                       texp, a.out, a.units);
-    TMR_CHECK_LAUNCH();
-    return TMR_OK;
-}
-
 // A-fragment prefetch distance (windows): 8 where the extra 16 (3-term) VGPRs
 // keep the occupancy -- the 2-row-quad, 3-group 3-term kernel (config E's
 // 32-row bands at 192 columns: 168 + 24 registers, 2 waves per SIMD either way

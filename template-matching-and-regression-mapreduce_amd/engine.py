@@ -844,7 +844,8 @@ class TMREngine:
         pc = prec_code(cfg.precision)
         choice = self.xcorr_algo
         if choice == "auto":  # measured per-k cost model (XCORR_COST)
-            fits = W % 64 == 0 and W <= 256 and mh <= 31 and mw <= 31 and (32 + mh // 2 * 2) * W <= 16384
+            # (xcorr.hip mfma_fits: a 32-row band, its halo and WIN_OVER = 3 rows staged in registers)
+            fits = W % 64 == 0 and W <= 256 and mh <= 31 and mw <= 31 and (35 + mh // 2 * 2) * W <= 16384
             choice = xcorr_choice(units["ht"], units["wt"], U / max(1, len(set(unit_image))), fits,
                                   one_term=pc != PREC_CODES["fp32"])
         self.last_xcorr_algo = choice

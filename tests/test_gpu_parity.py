@@ -1323,6 +1323,17 @@ def test_xcorr_mfma_refuses_other_widths():
         roi, ht, wt = oracle.template_size(boxes[u], H, W)
         ref = oracle.xcorr(f[0], oracle.roi_align(f[0], roi, ht, wt), 1.0)
         assert normwise(out[u].cpu().numpy(), ref) <= TOL
+    # 256 columns with a 31-row template: the band + halo + 3 over-rows exceed the
+    # MFMA kernel's staging registers, so 'auto' must pick the VALU kernel, not fail
+    W2 = 256
+    f2 = synth.normal(16, (1, C, H, W2))
+    boxes2 = np.stack([synth.exemplar_box(k, H, W2, 3, 9) for k in (31, 29)])
+    out2, _ = eng.match(cuda(f2), [0, 0], boxes2)
+    assert eng.last_xcorr_algo == "valu"
+    for u in range(2):
+        roi, ht, wt = oracle.template_size(boxes2[u], H, W2)
+        ref = oracle.xcorr(f2[0], oracle.roi_align(f2[0], roi, ht, wt), 1.0)
+        assert normwise(out2[u].cpu().numpy(), ref) <= TOL
 
 
 def test_xcorr_mfma_squeeze_and_engine():
