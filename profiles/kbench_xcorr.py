@@ -1,7 +1,8 @@
 """Micro-benchmark of the correlation kernel (tmr_xcorr) per template
 size and kernel: for each k, B images x E exemplars of k x k templates on
-fp [B,512,H,H]; HIP events around the xcorr launch on its stream (median of
-R repetitions).  One JSON line per (algo, k) with the SURVEY.md 8d roofline
+fp [B,512,H,H]; HIP events around the correlation kernel's launch on its stream
+(median of R repetitions; since round 6 the MFMA kernel's tmr_template_split
+pass is outside the events -- earlier rounds' kbench figures include it).  One JSON line per (algo, k) with the SURVEY.md 8d roofline
 figures: algorithmic bytes = read + write C*H*W fp32 per unit (fp read once
 per unit, f_TM written), FLOPs = 2*C*(H-k+1)^2*k^2 per unit; HBM peak 8 TB/s,
 fp32 VALU peak 157.3 TF.  --mixed runs the config-B mix (k uniform 3..15).
