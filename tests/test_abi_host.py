@@ -494,3 +494,20 @@ def test_graph_param_key_follows_the_parameter_dict():
     P["d"] = torch.zeros(1)
     assert [x[0] for x in e._param_key()] == ["a", "c", "d"]
 
+
+
+def test_toeplitz_table_matches_window_count():
+    """profiles/mfma_shapes/toeplitz.py (the round-6 shape study's useful-rate
+    table) prices the 2-D window form with the same window count the kernel
+    and the template split use (host.tsplit_windows)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "toeplitz", os.path.join(REPO, "profiles", "mfma_shapes", "toeplitz.py"))
+    tz = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tz)
+    for h in range(1, 32, 2):
+        for w in range(1, 32, 2):
+            assert tz.window_useful(w, h) == pytest.approx(h * w / (32.0 * host.tsplit_windows(h, w)))
+    # the row forms: w taps of a K-wide window per row, M outputs per block row
+    assert tz.row_useful(15, 16, 32) == pytest.approx(15 / 32)
+    assert tz.row_useful(19, 16, 32) == pytest.approx(19 / 64)
